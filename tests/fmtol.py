@@ -1,0 +1,82 @@
+"""Shared tolerances and golden loaders for the parity tests.
+
+Floating-point contract (BASELINE.json north star): FP64 slopes, t-stats and forecasts
+within 1e-9 relative error.  Relative to what: SURVEY.md §8(a) 'Tolerance definition' —
+|a-b| <= RTOL * max(|b|, s) with s = RMS of that coefficient's series, because a plain
+elementwise relative error is meaningless for slopes that happen to sit near zero.
+Integer outputs (N, month lists, masks, ranks) and winsorize cuts are compared bit-exact.
+"""
+import json
+import os
+
+import numpy as np
+
+RTOL = 1e-9
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load_npz(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def load_json(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def series_close(a, b, rtol=RTOL, scale=None):
+    """True if a ~ b under the series-RMS tolerance; NaN/inf must match exactly."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    if a.shape != b.shape:
+        return False
+    fin = np.isfinite(b)
+    if not np.array_equal(np.isnan(a), np.isnan(b)):
+        return False
+    if not np.array_equal(a[~fin & ~np.isnan(b)], b[~fin & ~np.isnan(b)]):
+        return False
+    if not fin.any():
+        return True
+    s = scale if scale is not None else float(np.sqrt(np.mean(b[fin] ** 2)))
+    tol = rtol * np.maximum(np.abs(b[fin]), s)
+    return bool(np.all(np.abs(a[fin] - b[fin]) <= tol))
+
+
+def assert_series_close(a, b, what="", rtol=RTOL, scale=None):
+    if not series_close(a, b, rtol, scale):
+        a = np.asarray(a, dtype=np.float64)
+        b = np.asarray(b, dtype=np.float64)
+        msg = f"{what}: shapes {a.shape} vs {b.shape}"
+        if a.shape == b.shape:
+            d = np.abs(a - b)
+            with np.errstate(invalid="ignore"):
+                i = int(np.nanargmax(d)) if np.isfinite(d).any() else 0
+            msg += f"; worst |diff|={d.flat[i]!r} at {i}: {a.flat[i]!r} vs {b.flat[i]!r}"
+        raise AssertionError(msg)
+
+
+def scalar_close(a, b, rtol=RTOL, scale=0.0):
+    if b is None:
+        return a is None or (isinstance(a, float) and np.isnan(a))
+    a = float(a)
+    if np.isinf(b) or np.isnan(b):
+        return a == b or (np.isnan(a) and np.isnan(b))
+    return abs(a - b) <= rtol * max(abs(b), scale)
+
+
+def frame_from(npz, prefix):
+    """Rebuild a DataFrame written by gen_goldens.frame_arrays (index + columns)."""
+    import pandas as pd
+    keys = [k for k in npz.files if k.startswith(prefix) and k != prefix + "index"]
+    data = {}
+    for k in keys:
+        c = k[len(prefix):]
+        v = npz[k]
+        if c == "mthcaldt":
+            v = v.astype("datetime64[ns]")
+        elif c == "primaryexch":
+            v = np.where(v == 1, "N", "Q")
+        elif c in ("is_all_but_tiny", "is_large"):
+            v = v.astype(bool)
+        data[c] = v
+    return pd.DataFrame(data, index=pd.Index(npz[prefix + "index"]))
