@@ -1,0 +1,214 @@
+"""Benchmark: the full Fama-MacBeth pass (BASELINE.json metric) on MI355X.
+
+Workload per GPU (BASELINE configs C3+C4): a 600-month x 5,000-firm synthetic panel with
+15 characteristics (retx + the 14 Lewellen predictors), generated in HBM by fm_gen_panel.
+One step = winsorize all 15 columns (1/99) -> NYSE me breakpoints + nested universes ->
+Models 1/2/3 x {All, All-but-tiny, Large} + the Figure-1 model x {All, Large} (11
+cross-sectional problems per month) in one batched Gram pass -> solves -> all-gather of
+the monthly records -> Fama-MacBeth means + Newey-West(4) -> 120/60 rolling means ->
+lagged-rolling forecasts + predictive-slope FM summaries.  Inputs are HBM-resident when
+the timed region starts.  With N GPUs (torchrun) each rank owns 600 months of a 600*N-month
+panel (weak scaling); value = all ranks' firm-month rows / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "fm-returnprediction_amd")
+for _p in (PKG, os.path.join(PKG, "src"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "firm-month rows/sec (and % HBM roofline) for full FM pass at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--months", type=int, default=600, help="months per GPU")
+    ap.add_argument("--firms", type=int, default=5000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-months", type=int, default=240, help="oracle CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify one step against the oracle")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from fmcore import dist as D
+    from fmcore import engine as E
+    from fmcore import lewellen as LW
+
+    cfg = LW.PipelineConfig()
+    model_cols = LW.table2_models()
+    T_loc, N = args.months, args.firms
+    T_glob = T_loc * world
+    panel = E.panel_synthetic(T_loc, N, args.seed, month0=rank * T_loc, device=dev)
+    rows_local = T_loc * N
+    seg_lo, seg_hi = rank * T_loc, (rank + 1) * T_loc
+    counts = [T_loc] * world
+
+    def step():
+        res, names, cuts, level, bp = LW.local_stage(panel, cfg, model_cols)
+        if world > 1:
+            rec_g, st_g = D.gather_records(res.rec, res.status, counts)
+            gres = E.FMResult(problems=res.problems, rec=rec_g, status=st_g, pmax=res.pmax,
+                              moments=res.moments, mom_stride=res.mom_stride)
+        else:
+            gres = res
+        ix, summ, roll, pred, pst = LW.time_series_stage(gres, cfg, moments=res.moments,
+                                                         seg_lo=seg_lo, seg_hi=seg_hi)
+        if world > 1:
+            pred, pst = D.combine_predictive(pred, pst)
+        psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
+        return gres, summ, psumm
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    timer = E.KernelTimer()
+    with timer:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    if world > 1:
+        dt = D.max_over_ranks(dt, dev)
+    gres, summ, psumm = out
+    nfit = int(((gres.status & 1) != 0).sum().item())
+
+    # roofline of the dominant kernel (per-launch algorithmic bytes / avg launch time)
+    C = panel.ncols
+    kern = {}
+    for tag in timer.names():
+        kern[tag] = timer.avg_ms(tag)
+    bytes_select = rows_local * C * 8            # one read of every winsorized column
+    bytes_gram = rows_local * (C * 8 + 1)         # every column + the universe level byte
+    cand = {"fm_select_cuts": bytes_select, "fm_gram": bytes_gram}
+    dom = max(cand, key=lambda k: kern.get(k, 0.0))
+    dom_ms = kern[dom]
+    achieved = cand[dom] / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(dom)
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": METRIC,
+        "value": rows_local * world * args.steps / dt,
+        "unit": "firm-month rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (counter-hash panel generated in HBM, Table-1 moments, t2 tails, 2% NaN)",
+        "config": {
+            "workload": "C3+C4 full pass per GPU: 600 months x 5000 firms x 15 chars; winsorize 1/99 -> "
+                        "NYSE universes -> M1/M2/M3 x 3 universes + Fig-1 x 2 -> NW(4) -> rolling 120/60 -> "
+                        "lagged-rolling forecasts + predictive-slope FM",
+            "months_per_gpu": T_loc, "firms": N, "chars": C, "problems_per_month": gres.nprob,
+            "global_months": T_glob, "parallelism": f"month-sharded x{world}, RCCL all-gather of records",
+        },
+        "regressions_per_s": nfit * args.steps / dt,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "bytes_per_launch": cand[dom], "avg_launch_ms": dom_ms},
+        "kernel_ms": {k: round(v, 4) for k, v in kern.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(panel, args, LW)
+    if args.check and rank == 0 and world == 1:
+        result["check"] = check_against_oracle(panel, gres, summ, args, LW)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def cpu_baseline(panel, args, LW):
+    """The CPU oracle (numpy restatement of the reference path; per-month SVD-pinv OLS,
+    numpy percentiles, NW, rolling) timed on a bounded month sample of the same panel."""
+    from oracle import fm_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    S = min(args.cpu_months, panel.nseg)
+    n = S * args.firms
+    cols = {name: panel.cols[i, :n].cpu().numpy() for i, name in enumerate(panel.names)}
+    me = panel.me[:n].cpu().numpy()
+    nyse = panel.nyse[:n].cpu().numpy().astype(bool)
+    seg = panel.seg_off_h[: S + 1]
+    models = {k: ("retx", v, (0, 1, 2)) for k, v in LW.table2_models().items()}
+    models["Figure 1"] = ("retx", LW.FIG1_VARS, (0, 2))
+    ctx = threadpool_limits(1) if threadpool_limits else None
+    t0 = time.perf_counter()
+    if ctx:
+        with ctx:
+            O.pipeline_arrays(cols, seg, me, nyse, models, None)
+    else:
+        O.pipeline_arrays(cols, seg, me, nyse, models, None)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "firm-month rows/s", "cores": 1, "kind": "port",
+            "seconds": dt,
+            "sample": f"first {S} months x {args.firms} firms of the same panel, full pass "
+                      f"(11 problems/month, rolling, forecasts), oracle/fm_oracle.py, 1 BLAS thread"}
+
+
+def check_against_oracle(panel, gres, summ, args, LW):
+    """Spot check: monthly records of 3 months against the oracle on those months."""
+    from oracle import fm_oracle as O
+    S = 3
+    n = S * args.firms
+    cols = {name: panel.cols[i, :n].cpu().numpy() for i, name in enumerate(panel.names)}
+    models = {k: ("retx", v, (0, 1, 2)) for k, v in LW.table2_models().items()}
+    ref = O.pipeline_arrays(cols, panel.seg_off_h[: S + 1], panel.me[:n].cpu().numpy(),
+                            panel.nyse[:n].cpu().numpy().astype(bool), models, None)
+    rec = gres.rec.cpu().numpy()
+    worst = 0.0
+    for k, p in enumerate(gres.problems):
+        if p.model >= 3:
+            continue
+        name = list(models)[p.model]
+        r = ref[(name, p.level)]
+        for i, t in enumerate(r["month"]):
+            a = rec[t, k, : p.K + 1]
+            b = r["params"][i]
+            worst = max(worst, float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-3))))
+    return {"months": S, "worst_rel_param_err": worst}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+// Shared device/host helpers for libfm_hip (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fm_hip.h"
+
+namespace fm {
+
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define FM_REQUIRE(cond, ...)            \
+    do {                                 \
+        if (!(cond)) {                   \
+            ::fm::set_error(__VA_ARGS__); \
+            return FM_EINVAL;            \
+        }                                \
+    } while (0)
+
+#define FM_CHECK_LAUNCH(name)                       \
+    do {                                            \
+        int rc_ = ::fm::check_launch(name);         \
+        if (rc_ != FM_OK) return rc_;               \
+    } while (0)
+
+constexpr uint64_t SENT = ~0ull;   // key of NaN / absent values: sorts after +inf
+constexpr int WAVE = 64;
+
+// Order-preserving map double -> uint64 (total order with -0.0 < +0.0; callers map NaN
+// to SENT before calling).
+__device__ __forceinline__ uint64_t dkey(double v) {
+    uint64_t b = (uint64_t)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double kval(uint64_t k) {
+    uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    return __longlong_as_double((long long)b);
+}
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// number of set bits of `mask` strictly below this lane
+__device__ __forceinline__ int mask_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint64_t w = (uint64_t)__shfl_xor((long long)v, o, WAVE);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint64_t w = (uint64_t)__shfl_xor((long long)v, o, WAVE);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, WAVE);
+    return v;
+}
+
+// Block-wide reductions for blocks of NW waves; `scratch` holds NW elements.  Every
+// thread of the block must call; result is returned to all threads.
+template <int NW, typename T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+    v = wave_sum(v);
+    const int w = threadIdx.x / WAVE;
+    __syncthreads();
+    if (lane_id() == 0) scratch[w] = v;
+    __syncthreads();
+    T s = scratch[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s += scratch[i];
+    return s;
+}
+template <int NW>
+__device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* scratch) {
+    v = wave_min_u64(v);
+    const int w = threadIdx.x / WAVE;
+    __syncthreads();
+    if (lane_id() == 0) scratch[w] = v;
+    __syncthreads();
+    uint64_t s = scratch[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s = scratch[i] < s ? scratch[i] : s;
+    return s;
+}
+template <int NW>
+__device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t* scratch) {
+    v = wave_max_u64(v);
+    const int w = threadIdx.x / WAVE;
+    __syncthreads();
+    if (lane_id() == 0) scratch[w] = v;
+    __syncthreads();
+    uint64_t s = scratch[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s = scratch[i] > s ? scratch[i] : s;
+    return s;
+}
+
+// Exclusive prefix sum over the block (NW waves); returns this thread's offset and the
+// block total via *total.
+template <int NW>
+__device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) {
+    const int lane = lane_id();
+    const int w = threadIdx.x / WAVE;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        int y = __shfl_up(x, o, WAVE);
+        if (lane >= o) x += y;
+    }
+    __syncthreads();
+    if (lane == WAVE - 1) scratch[w] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        int s = scratch[i];
+        if (i < w) base += s;
+        tot += s;
+    }
+    *total = tot;
+    return base + x - v;
+}
+
+}  // namespace fm

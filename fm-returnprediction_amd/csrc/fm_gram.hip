@@ -1,0 +1,264 @@
+// fm_gram: clip -> dropna-validity -> shifted Gram accumulation on FP64 MFMA.
+//
+// Replaces, for every (month, model, universe) problem at once, the row filtering of
+// run_monthly_cs_regressions (`.dropna()`, reference src/regressions.py:39), the universe
+// subsetting of get_subsets (src/calc_Lewellen_2014.py:95-105) and the X'X / X'y / y'y
+// formation inside sm.OLS (src/regressions.py:57, src/calc_Lewellen_2014.py:917-919).
+//
+// Data flow per workgroup (one chunk of one month; 256 threads = 4 waves):
+//   1. each thread streams one row of the chunk tile: ncols coalesced FP64 loads (one per
+//      column, SoA), clip to the month's winsorize cuts, NaN/inf tests, shift by the
+//      month's pivot (optional standardize scale), z = [1, x..., y] with NaN -> 0;
+//   2. the row's validity pattern (bit m: every column model m needs is non-NaN) and its
+//      universe level give a bucket id; a wave-ballot counting sort scatters the tile
+//      into LDS grouped by bucket, each bucket padded to a multiple of 4 rows;
+//   3. each wave walks 4-row groups of the sorted tile and issues
+//      v_mfma_f64_16x16x4_f64 with A = B = the group's z rows (lane l holds
+//      z[row l>>4][col l&15]), accumulating Z^T Z per bucket in registers (16x16 FP64
+//      tile = 4 doubles per lane; two tiles wide for up to 31 columns).
+// At chunk end the four waves' accumulators are summed through LDS and written as one
+// zw*zw Gram per (chunk, bucket).  fm_solve combines buckets into problems: model m's
+// Gram is the sum over patterns that contain m and levels >= the problem's universe,
+// restricted to m's columns.  One HBM read of the panel serves every model x universe.
+#include <math.h>
+
+#include "fm_common.h"
+
+namespace fm {
+namespace {
+
+constexpr int GT = 256;
+constexpr int GNW = GT / WAVE;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+template <int NT, int NB, int MINW>
+__global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
+    constexpr int ZW = 16 * NT;
+    constexpr int RS = ZW + 1;          // LDS row stride (doubles): conflict-free scatter
+    constexpr int ROWS = GT + 3 * NB;   // sorted tile incl. padding rows
+    constexpr int TILE = ROWS * RS > GNW * ZW * ZW ? ROWS * RS : GNW * ZW * ZW;
+    __shared__ double tile[TILE];
+    __shared__ double prm[4][32];
+    __shared__ int wcnt[GNW][NB];
+    __shared__ int woff[GNW][NB];
+    __shared__ int boff[NB + 1];
+    __shared__ int btot[NB];
+    __shared__ uint8_t lut[64];
+    __shared__ uint32_t mmask[FM_MAX_MODELS], ymask[FM_MAX_MODELS];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1);
+    const int w = tid / WAVE;
+    const int chunk = blockIdx.x;
+    const int seg = a.chunk_seg[chunk];
+    const int64_t r0 = a.chunk_row[2 * chunk], r1 = a.chunk_row[2 * chunk + 1];
+    const int ncols = a.ncols, nseg = a.nseg, nmodels = a.nmodels, nlevels = a.nlevels;
+
+    for (int c = tid; c < 32; c += GT) {
+        const bool on = c < ncols;
+        const int64_t o = (int64_t)c * nseg + seg;
+        prm[0][c] = (on && a.lo) ? a.lo[o] : NAN;
+        prm[1][c] = (on && a.hi) ? a.hi[o] : NAN;
+        prm[2][c] = (on && a.shift) ? a.shift[o] : 0.0;
+        prm[3][c] = (on && a.inv_scale) ? a.inv_scale[o] : 1.0;
+    }
+    for (int i = tid; i < (1 << nmodels); i += GT) lut[i] = a.pattern_id[i];
+    if (tid < nmodels) {
+        mmask[tid] = a.model_mask[tid];
+        ymask[tid] = a.model_ymask[tid];
+    }
+    __syncthreads();
+
+    d4 acc0[NB], acc1[NB], acc2[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        acc0[b] = d4{0.0, 0.0, 0.0, 0.0};
+        if (NT == 2) {
+            acc1[b] = d4{0.0, 0.0, 0.0, 0.0};
+            acc2[b] = d4{0.0, 0.0, 0.0, 0.0};
+        }
+    }
+    uint32_t fl = 0;   // bit 2m: inf in a regressor of model m; bit 2m+1: inf in its y
+
+    for (int64_t t0 = r0; t0 < r1; t0 += GT) {
+        const int64_t row = t0 + tid;
+        const bool inr = row < r1;
+        double z[ZW];
+        z[0] = 1.0;
+        uint32_t nn = 0, infb = 0;
+#pragma unroll
+        for (int c = 0; c < ZW - 1; ++c) {
+            double v = 0.0;
+            if (c < ncols && inr) {
+                double x = a.cols[(int64_t)c * a.col_stride + row];
+                const double l = prm[0][c], h = prm[1][c];
+                if (x < l) x = l;   // pandas clip semantics: NaN stays, NaN bound ignored
+                if (x > h) x = h;
+                if (!isnan(x)) {
+                    nn |= 1u << c;
+                    if (isinf(x)) infb |= 1u << c;
+                    v = (x - prm[2][c]) * prm[3][c];
+                }
+            }
+            z[1 + c] = v;
+        }
+        uint32_t pat = 0;
+        for (int m = 0; m < nmodels; ++m)
+            if ((nn & mmask[m]) == mmask[m]) pat |= 1u << m;
+        const int pid = inr ? (int)lut[pat] : 255;
+        int bucket = -1;
+        if (pid != 255) {
+            int lvl = a.level ? (int)a.level[row] : 0;
+            lvl = lvl < nlevels ? lvl : nlevels - 1;
+            bucket = pid * nlevels + lvl;
+        }
+        if (infb != 0 && bucket >= 0) {
+            for (int m = 0; m < nmodels; ++m) {
+                if (!((pat >> m) & 1u)) continue;
+                if (infb & mmask[m] & ~ymask[m]) fl |= 1u << (2 * m);
+                if (infb & ymask[m]) fl |= 1u << (2 * m + 1);
+            }
+        }
+        // ---- counting sort of the tile by bucket (wave ballots; deterministic order)
+        int rank = 0;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const uint64_t mb = __ballot(bucket == b);
+            if (bucket == b) rank = mask_rank(mb);
+            if (lane == 0) wcnt[w][b] = __popcll(mb);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int off = 0;
+            for (int b = 0; b < NB; ++b) {
+                int tot = 0;
+                for (int ww = 0; ww < GNW; ++ww) {
+                    woff[ww][b] = off + tot;
+                    tot += wcnt[ww][b];
+                }
+                btot[b] = tot;
+                boff[b] = off;
+                off += (tot + 3) & ~3;
+            }
+            boff[NB] = off;
+        }
+        __syncthreads();
+        if (bucket >= 0) {
+            double* dst = tile + (woff[w][bucket] + rank) * RS;
+#pragma unroll
+            for (int c = 0; c < ZW; ++c) dst[c] = z[c];
+        }
+        if (tid < NB * 3) {
+            const int b = tid / 3, k = tid - 3 * (tid / 3);
+            const int rp = boff[b] + btot[b] + k;
+            if (rp < boff[b + 1]) {
+#pragma unroll
+                for (int c = 0; c < ZW; ++c) tile[rp * RS + c] = 0.0;
+            }
+        }
+        __syncthreads();
+        // ---- MFMA accumulation, one bucket at a time (static register indices)
+        const int col = lane & 15, sub = lane >> 4;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int g1 = boff[b + 1] >> 2;
+            for (int g = (boff[b] >> 2) + w; g < g1; g += GNW) {
+                const double* rp = tile + (4 * g + sub) * RS;
+                const double a0 = rp[col];
+                acc0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a0, acc0[b], 0, 0, 0);
+                if (NT == 2) {
+                    const double a1 = rp[16 + col];
+                    acc1[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a1, acc1[b], 0, 0, 0);
+                    acc2[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, a1, acc2[b], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- inf flags (rare): one atomic per wave per model
+    const uint32_t wf = wave_or_u32(fl);
+    if (lane == 0 && wf != 0) {
+        for (int m = 0; m < nmodels; ++m) {
+            uint32_t bits = 0;
+            if ((wf >> (2 * m)) & 1u) bits |= FM_ST_INF_IN_X;
+            if ((wf >> (2 * m + 1)) & 1u) bits |= FM_ST_INF_IN_Y;
+            if (bits) atomicOr(&a.flags[(int64_t)seg * nmodels + m], bits);
+        }
+    }
+
+    // ---- cross-wave reduction and store: partial[chunk][bucket][ZW][ZW]
+    const int nbr = a.npatterns * nlevels;
+    double* outp = a.partial + (int64_t)chunk * nbr * ZW * ZW;
+    const int col = lane & 15, sub = lane >> 4;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b >= nbr) continue;   // block-uniform
+        double* red = tile + w * ZW * ZW;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = sub + 4 * r;
+            red[i * ZW + col] = acc0[b][r];
+            if (NT == 2) {
+                red[i * ZW + 16 + col] = acc1[b][r];
+                red[(16 + col) * ZW + i] = acc1[b][r];
+                red[(16 + i) * ZW + 16 + col] = acc2[b][r];
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < ZW * ZW; e += GT) {
+            double s = tile[e];
+#pragma unroll
+            for (int ww = 1; ww < GNW; ++ww) s += tile[ww * ZW * ZW + e];
+            outp[(int64_t)b * ZW * ZW + e] = s;
+        }
+        __syncthreads();
+    }
+}
+
+template <int NT, int NB, int MINW>
+void launch_gram(const fm_gram_args& a, hipStream_t st) {
+    hipLaunchKernelGGL((gram_kernel<NT, NB, MINW>), dim3(a.nchunks), dim3(GT), 0, st, a);
+}
+
+}  // namespace
+}  // namespace fm
+
+extern "C" int fm_gram(const fm_gram_args* args, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(args != nullptr, "fm_gram: null args");
+    const fm_gram_args& a = *args;
+    FM_REQUIRE(a.cols && a.seg_off && a.chunk_seg && a.chunk_row && a.partial && a.flags &&
+                   a.model_mask && a.model_ymask && a.pattern_id,
+               "fm_gram: null pointer");
+    FM_REQUIRE(a.ncols >= 1 && a.ncols <= FM_MAX_COLS, "fm_gram: ncols must be 1..%d", FM_MAX_COLS);
+    FM_REQUIRE(a.nmodels >= 1 && a.nmodels <= FM_MAX_MODELS, "fm_gram: nmodels must be 1..%d",
+               FM_MAX_MODELS);
+    FM_REQUIRE(a.nlevels >= 1 && a.nlevels <= FM_MAX_LEVELS, "fm_gram: nlevels must be 1..%d",
+               FM_MAX_LEVELS);
+    FM_REQUIRE(a.npatterns >= 1, "fm_gram: npatterns must be >= 1");
+    if (a.nchunks == 0) return FM_OK;
+    const int nb = a.npatterns * a.nlevels;
+    hipStream_t st = (hipStream_t)stream;
+    if (a.ncols <= 15) {
+        if (nb <= 1) launch_gram<1, 1, 2>(a, st);
+        else if (nb <= 4) launch_gram<1, 4, 2>(a, st);
+        else if (nb <= 8) launch_gram<1, 8, 2>(a, st);
+        else if (nb <= 16) launch_gram<1, 16, 2>(a, st);
+        else {
+            set_error("fm_gram: %d buckets exceed 16 for <=15 columns", nb);
+            return FM_ETOOBIG;
+        }
+    } else {
+        if (nb <= 1) launch_gram<2, 1, 2>(a, st);
+        else if (nb <= 4) launch_gram<2, 4, 2>(a, st);
+        else if (nb <= 8) launch_gram<2, 8, 1>(a, st);
+        else {
+            set_error("fm_gram: %d buckets exceed 8 for >15 columns", nb);
+            return FM_ETOOBIG;
+        }
+    }
+    FM_CHECK_LAUNCH("fm_gram");
+    return FM_OK;
+}

@@ -1,0 +1,327 @@
+// fm_solve: per (month, model, universe) OLS from the bucketed shifted Grams.
+//
+// Replaces sm.OLS(Y, X).fit() -> params / rsquared / N and the N < K+1 month skip of
+// run_monthly_cs_regressions (reference src/regressions.py:52-72) and the create_figure_1
+// OLS (src/calc_Lewellen_2014.py:913-921).  statsmodels solves with an SVD pseudo-inverse
+// of X; here the slopes come from the centered normal equations
+//     Sxx b = Sxy,  Sxx = sum (x-xbar)(x-xbar)', Sxy = sum (x-xbar)(y-ybar)
+// by a Cholesky factorization (one wavefront per problem, lanes over matrix entries).
+// When a pivot collapses (1 - R^2 of a regressor on the previous ones <= 1e-9, e.g. an
+// all-zero column or an exactly collinear pair) the wave falls back to a Jacobi
+// eigen-decomposition of Sxx and the minimum-norm (pseudo-inverse) solution, which is
+// what statsmodels' pinv returns when the null space does not involve the intercept.
+// R^2 = 1 - (Syy - b'Sxy)/Syy (centered TSS: the model has a constant).
+//
+// One workgroup (4 waves) per month: the month's bucket Grams are first summed over its
+// chunks into LDS, then the waves take the month's problems round-robin.
+#include <math.h>
+
+#include "fm_common.h"
+
+namespace fm {
+namespace {
+
+constexpr int VT = 256;
+constexpr int VNW = VT / WAVE;
+constexpr int MAXB_LDS = 8192;   // doubles of bucket sums held in LDS (64 KB)
+constexpr double CHOL_REL = 1e-9;
+constexpr double EIG_REL = 1e-12;
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+struct WaveScratch {
+    double A[32 * 32];   // G, then L (Cholesky) or the Jacobi matrix
+    double V[32 * 32];   // centered S, then Jacobi eigenvectors
+    double sxy[32], sdiag[32], mu[32], b[32], misc[8];
+};
+
+// Cyclic Jacobi + pseudo-inverse solve by lane 0 (rare fallback path).
+__device__ void jacobi_pinv(double* A, double* V, int K, const double* sxy, double* b) {
+    for (int i = 0; i < K; ++i)
+        for (int j = 0; j < K; ++j) V[i * 32 + j] = i == j ? 1.0 : 0.0;
+    double frob = 0.0;
+    for (int i = 0; i < K; ++i)
+        for (int j = 0; j < K; ++j) frob += A[i * 32 + j] * A[i * 32 + j];
+    for (int sweep = 0; sweep < 80; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < K; ++p)
+            for (int q = p + 1; q < K; ++q) off += A[p * 32 + q] * A[p * 32 + q];
+        if (off <= 1e-34 * frob) break;
+        for (int p = 0; p < K; ++p) {
+            for (int q = p + 1; q < K; ++q) {
+                const double apq = A[p * 32 + q];
+                if (apq == 0.0) continue;
+                const double theta = (A[q * 32 + q] - A[p * 32 + p]) / (2.0 * apq);
+                const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < K; ++k) {
+                    const double akp = A[k * 32 + p], akq = A[k * 32 + q];
+                    A[k * 32 + p] = c * akp - s * akq;
+                    A[k * 32 + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < K; ++k) {
+                    const double apk = A[p * 32 + k], aqk = A[q * 32 + k];
+                    A[p * 32 + k] = c * apk - s * aqk;
+                    A[q * 32 + k] = s * apk + c * aqk;
+                }
+                A[p * 32 + q] = 0.0;
+                A[q * 32 + p] = 0.0;
+                for (int k = 0; k < K; ++k) {
+                    const double vkp = V[k * 32 + p], vkq = V[k * 32 + q];
+                    V[k * 32 + p] = c * vkp - s * vkq;
+                    V[k * 32 + q] = s * vkp + c * vkq;
+                }
+            }
+        }
+    }
+    double lmax = 0.0;
+    for (int i = 0; i < K; ++i) lmax = fmax(lmax, fabs(A[i * 32 + i]));
+    for (int j = 0; j < K; ++j) b[j] = 0.0;
+    for (int i = 0; i < K; ++i) {
+        const double l = A[i * 32 + i];
+        if (!(l > EIG_REL * lmax)) continue;
+        double proj = 0.0;
+        for (int k = 0; k < K; ++k) proj += V[k * 32 + i] * sxy[k];
+        proj /= l;
+        for (int j = 0; j < K; ++j) b[j] += proj * V[j * 32 + i];
+    }
+}
+
+__global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
+    __shared__ double bs[MAXB_LDS];
+    __shared__ WaveScratch ws_all[VNW];
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+    const int zw = a.zw, zz = zw * zw;
+    const int nb = a.npatterns * a.nlevels;
+    const int c0 = a.seg_chunk_off[s], c1 = a.seg_chunk_off[s + 1];
+    for (int e = tid; e < nb * zz; e += VT) {
+        double acc = 0.0;
+        for (int c = c0; c < c1; ++c) acc += a.partial[(int64_t)c * nb * zz + e];
+        bs[e] = acc;
+    }
+    __syncthreads();
+    WaveScratch& ws = ws_all[w];
+    const int rs = a.pmax + 2;
+    for (int p = w; p < a.nprob; p += VNW) {
+        const int m = a.prob_model[p], u = a.prob_level[p], nz = a.prob_nz[p];
+        const int* zi = a.prob_z + p * 32;
+        const int K = nz - 2;
+        // ---- assemble the problem Gram G[i][j] over its buckets
+        for (int e = lane; e < nz * nz; e += WAVE) {
+            const int i = e / nz, j = e - (e / nz) * nz;
+            const int off = zi[i] * zw + zi[j];
+            double acc = 0.0;
+            for (int b = 0; b < nb; ++b) {
+                const int pid = b / a.nlevels, lvl = b - pid * a.nlevels;
+                if (((a.pattern_models[pid] >> m) & 1u) && lvl >= u) acc += bs[b * zz + off];
+            }
+            ws.A[i * 32 + j] = acc;
+        }
+        wave_sync();
+        const double n = ws.A[0];
+        const int64_t ro = ((int64_t)s * a.nprob + p) * rs;
+        uint32_t st = 0;
+        if (a.gram_flags) st |= a.gram_flags[(int64_t)s * a.nmodels + m] & (FM_ST_INF_IN_X | FM_ST_INF_IN_Y);
+        if (!(n >= (double)(K + 1))) {
+            for (int k = lane; k < rs; k += WAVE) a.rec[ro + k] = k == a.pmax + 1 ? n : NAN;
+            if (lane == 0) a.status[(int64_t)s * a.nprob + p] = FM_ST_SKIPPED;
+            wave_sync();
+            continue;
+        }
+        // ---- centered moments S over (x_1..x_K, y)
+        const int K1 = K + 1;
+        for (int e = lane; e < K1 * K1; e += WAVE) {
+            const int i = e / K1, j = e - (e / K1) * K1;
+            ws.V[i * 32 + j] = ws.A[(1 + i) * 32 + 1 + j] - ws.A[1 + i] * ws.A[1 + j] / n;
+        }
+        if (lane < K1) ws.mu[lane] = ws.A[1 + lane] / n;
+        if (lane < K) {
+            const double sd = ws.A[(1 + lane) * 32 + 1 + lane];
+            ws.sdiag[lane] = sd;   // raw (shifted) second moment, for the constant test
+        }
+        wave_sync();
+        if (lane < K) ws.sxy[lane] = ws.V[lane * 32 + K];
+        if (a.moments) {
+            double* mo = a.moments + ((int64_t)s * a.nprob + p) * a.mom_stride;
+            if (lane == 0) mo[0] = n;
+            if (lane < K1) mo[1 + lane] = ws.mu[lane];
+            for (int e = lane; e < K1 * K1; e += WAVE)
+                mo[1 + K1 + e] = ws.V[(e / K1) * 32 + (e - (e / K1) * K1)];
+        }
+        const double syy = ws.V[K * 32 + K];
+        if ((a.prob_flags[p] & 1) != 0) {
+            bool sus = false;
+            if (lane < K) {
+                const double v = ws.V[lane * 32 + lane];
+                sus = !(v > 1e-10 * ws.sdiag[lane]);
+            }
+            if (__ballot(sus) != 0) st |= FM_ST_CONST_SUSPECT;
+        }
+        // ---- Cholesky of Sxx (in A)
+        for (int e = lane; e < K * K; e += WAVE) {
+            const int i = e / K, j = e - (e / K) * K;
+            ws.A[i * 32 + j] = ws.V[i * 32 + j];
+        }
+        wave_sync();
+        bool ok = true;
+        for (int k = 0; k < K; ++k) {
+            const double piv = ws.A[k * 32 + k];
+            const double orig = ws.V[k * 32 + k];
+            if (!(orig > 0.0) || !(piv > CHOL_REL * orig)) {
+                ok = false;
+                break;
+            }
+            const double lkk = sqrt(piv);
+            wave_sync();
+            if (lane > k && lane < K) ws.A[lane * 32 + k] /= lkk;
+            if (lane == k) ws.A[k * 32 + k] = lkk;
+            wave_sync();
+            const int mrem = K - k - 1;
+            for (int e = lane; e < mrem * mrem; e += WAVE) {
+                const int i = k + 1 + e / mrem, j = k + 1 + (e - (e / mrem) * mrem);
+                if (j <= i) ws.A[i * 32 + j] -= ws.A[i * 32 + k] * ws.A[j * 32 + k];
+            }
+            wave_sync();
+        }
+        if (ok) {
+            if (lane == 0) {
+                double* y = ws.b;
+                for (int i = 0; i < K; ++i) {
+                    double t = ws.sxy[i];
+                    for (int j = 0; j < i; ++j) t -= ws.A[i * 32 + j] * y[j];
+                    y[i] = t / ws.A[i * 32 + i];
+                }
+                for (int i = K - 1; i >= 0; --i) {
+                    double t = y[i];
+                    for (int j = i + 1; j < K; ++j) t -= ws.A[j * 32 + i] * y[j];
+                    y[i] = t / ws.A[i * 32 + i];
+                }
+            }
+        } else {
+            st |= FM_ST_RANK_DEF;
+            for (int e = lane; e < K * K; e += WAVE) {
+                const int i = e / K, j = e - (e / K) * K;
+                ws.A[i * 32 + j] = ws.V[i * 32 + j];
+            }
+            wave_sync();
+            if (lane == 0) jacobi_pinv(ws.A, ws.V, K, ws.sxy, ws.b);
+        }
+        wave_sync();
+        if (lane == 0) {
+            double bsxy = 0.0;
+            for (int j = 0; j < K; ++j) bsxy += ws.b[j] * ws.sxy[j];
+            const double r2 = 1.0 - (syy - bsxy) / syy;
+            double icpt = ws.mu[K];
+            for (int j = 0; j < K; ++j) icpt -= ws.b[j] * ws.mu[j];
+            if (a.add_back) {
+                icpt += a.add_back[(int64_t)(zi[K + 1] - 1) * a.nseg + s];
+                for (int j = 0; j < K; ++j) icpt -= ws.b[j] * a.add_back[(int64_t)(zi[1 + j] - 1) * a.nseg + s];
+            }
+            ws.misc[0] = r2;
+            ws.misc[1] = icpt;
+        }
+        wave_sync();
+        for (int k = lane; k < rs; k += WAVE) {
+            double v = NAN;
+            if (k == 0) v = ws.misc[1];
+            else if (k <= K) v = ws.b[k - 1];
+            else if (k == a.pmax) v = ws.misc[0];
+            else if (k == a.pmax + 1) v = n;
+            a.rec[ro + k] = v;
+        }
+        if (lane == 0) a.status[(int64_t)s * a.nprob + p] = st | FM_ST_FITTED;
+        wave_sync();
+    }
+}
+
+// Exact nonzero-constant test for problems flagged CONST_SUSPECT (statsmodels
+// add_constant(has_constant='skip'): np.ptp(x)==0 & all(x != 0), src/regressions.py:50).
+__global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t stride, int ncols,
+                                                   const int64_t* seg_off, int nseg,
+                                                   const double* lo, const double* hi,
+                                                   const uint8_t* level, int nprob,
+                                                   const int32_t* prob_level, const int32_t* prob_z,
+                                                   const int32_t* prob_nz, const int32_t* pairs,
+                                                   uint32_t* status) {
+    __shared__ uint64_t red[VNW];
+    const int s = pairs[2 * blockIdx.x], p = pairs[2 * blockIdx.x + 1];
+    const int nz = prob_nz[p], K = nz - 2, u = prob_level[p];
+    const int* zi = prob_z + p * 32;
+    const int64_t r0 = seg_off[s], r1 = seg_off[s + 1];
+    bool any_const = false;
+    for (int j = 0; j < K; ++j) {
+        const int cx = zi[1 + j] - 1;
+        uint64_t kmin = SENT, kmax = 0;
+        bool allnz = true;
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += VT) {
+            if (level && (int)level[r] < u) continue;
+            bool ok = true;
+            double xv = 0.0;
+            for (int q = 1; q < nz; ++q) {
+                const int c = zi[q] - 1;
+                double x = cols[(int64_t)c * stride + r];
+                if (lo) {
+                    const double l = lo[(int64_t)c * nseg + s], h = hi[(int64_t)c * nseg + s];
+                    if (x < l) x = l;
+                    if (x > h) x = h;
+                }
+                if (isnan(x)) ok = false;
+                if (c == cx) xv = x;
+            }
+            if (!ok) continue;
+            const uint64_t k = dkey(xv == 0.0 ? 0.0 : xv);
+            kmin = k < kmin ? k : kmin;
+            kmax = k > kmax ? k : kmax;
+            if (xv == 0.0) allnz = false;
+        }
+        kmin = block_min_u64<VNW>(kmin, red);
+        kmax = block_max_u64<VNW>(kmax, red);
+        const int nzr = block_sum<VNW>(allnz ? 0 : 1, (int*)red);
+        if (kmin != SENT && kmin == kmax && nzr == 0) any_const = true;
+    }
+    if (threadIdx.x == 0 && any_const) status[(int64_t)s * nprob + p] |= FM_ST_CONST_COL;
+}
+
+}  // namespace
+}  // namespace fm
+
+extern "C" int fm_solve(const fm_solve_args* args, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(args != nullptr, "fm_solve: null args");
+    const fm_solve_args& a = *args;
+    FM_REQUIRE(a.partial && a.seg_chunk_off && a.pattern_models && a.prob_model && a.prob_level &&
+                   a.prob_z && a.prob_nz && a.prob_flags && a.rec && a.status,
+               "fm_solve: null pointer");
+    FM_REQUIRE(a.zw == 16 || a.zw == 32, "fm_solve: zw must be 16 or 32");
+    FM_REQUIRE(a.npatterns * a.nlevels * a.zw * a.zw <= MAXB_LDS,
+               "fm_solve: %d buckets x %d^2 exceed the LDS budget", a.npatterns * a.nlevels, a.zw);
+    FM_REQUIRE(a.pmax >= 2 && a.pmax <= 32, "fm_solve: pmax must be 2..32");
+    FM_REQUIRE(a.moments == nullptr || a.mom_stride > 0, "fm_solve: bad mom_stride");
+    if (a.nseg == 0 || a.nprob == 0) return FM_OK;
+    hipLaunchKernelGGL(solve_kernel, dim3(a.nseg), dim3(VT), 0, (hipStream_t)stream, a);
+    FM_CHECK_LAUNCH("fm_solve");
+    return FM_OK;
+}
+
+extern "C" int fm_const_check(const double* cols, int64_t col_stride, int32_t ncols,
+                              const int64_t* seg_off, int32_t nseg, const double* lo,
+                              const double* hi, const uint8_t* level, int32_t nprob,
+                              const int32_t* prob_level, const int32_t* prob_z,
+                              const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
+                              uint32_t* status, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(cols && seg_off && prob_level && prob_z && prob_nz && pairs && status,
+               "fm_const_check: null pointer");
+    FM_REQUIRE((lo == nullptr) == (hi == nullptr), "fm_const_check: lo/hi must both be set or NULL");
+    if (npairs == 0) return FM_OK;
+    hipLaunchKernelGGL(const_kernel, dim3(npairs), dim3(VT), 0, (hipStream_t)stream, cols,
+                       col_stride, ncols, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
+                       prob_nz, pairs, status);
+    FM_CHECK_LAUNCH("fm_const_check");
+    return FM_OK;
+}

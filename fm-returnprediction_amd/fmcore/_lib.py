@@ -1,0 +1,121 @@
+"""ctypes binding of libfm_hip.so (include/fm_hip.h).
+
+The shared library is built in-tree (``fm-returnprediction_amd/lib/libfm_hip.so``, see
+``csrc/Makefile`` / ``__graft_entry__.build()``).  There is no fallback: if the library is
+missing, or no HIP device is present when a compute entry point is used, this module
+raises.  All pointer arguments are device pointers taken from torch tensors.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("FM_HIP_LIB", os.path.join(_PKG_DIR, "lib", "libfm_hip.so"))
+
+FM_ST_FITTED = 0x1
+FM_ST_SKIPPED = 0x2
+FM_ST_INF_IN_X = 0x4
+FM_ST_INF_IN_Y = 0x8
+FM_ST_CONST_SUSPECT = 0x10
+FM_ST_CONST_COL = 0x20
+FM_ST_RANK_DEF = 0x40
+
+FM_MAX_COLS = 31
+FM_MAX_MODELS = 6
+FM_MAX_LEVELS = 3
+
+_p = C.c_void_p
+_i32 = C.c_int32
+_i64 = C.c_int64
+_f64 = C.c_double
+
+
+class GramArgs(C.Structure):
+    _fields_ = [
+        ("cols", _p), ("col_stride", _i64), ("ncols", _i32), ("nseg", _i32),
+        ("seg_off", _p), ("chunk_seg", _p), ("chunk_row", _p), ("nchunks", _i32),
+        ("lo", _p), ("hi", _p), ("shift", _p), ("inv_scale", _p),
+        ("level", _p), ("nlevels", _i32),
+        ("model_mask", _p), ("model_ymask", _p), ("nmodels", _i32),
+        ("pattern_id", _p), ("npatterns", _i32),
+        ("partial", _p), ("flags", _p),
+    ]
+
+
+class SolveArgs(C.Structure):
+    _fields_ = [
+        ("partial", _p), ("seg_chunk_off", _p), ("nseg", _i32), ("zw", _i32),
+        ("nlevels", _i32), ("npatterns", _i32), ("pattern_models", _p),
+        ("nprob", _i32), ("prob_model", _p), ("prob_level", _p), ("prob_z", _p),
+        ("prob_nz", _p), ("prob_flags", _p), ("add_back", _p), ("gram_flags", _p),
+        ("nmodels", _i32), ("pmax", _i32), ("rec", _p), ("status", _p),
+        ("moments", _p), ("mom_stride", _i32),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "fm_version": (C.c_char_p, []),
+    "fm_last_error": (C.c_char_p, []),
+    "fm_device_arch": (_i32, [C.c_char_p, _i32]),
+    "fm_abi_sizes": (_i32, [C.POINTER(_i32), C.POINTER(_i32)]),
+    "fm_select_cuts": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _f64, _f64, _i32, _i32,
+                              _p, _p, _p, _p, _p, _p]),
+    "fm_clip": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
+    "fm_standardize": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
+    "fm_universe_level": (_i32, [_p, _p, _i32, _i64, _p, _p, _p, _p]),
+    "fm_pilot_shift": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p]),
+    "fm_gram": (_i32, [C.POINTER(GramArgs), _p]),
+    "fm_solve": (_i32, [C.POINTER(SolveArgs), _p]),
+    "fm_const_check": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _i32, _p, _p, _p, _p,
+                              _i32, _p, _p]),
+    "fm_ts_compact": (_i32, [_p, _i64, _i64, _i32, _i32, _p, _p, _p]),
+    "fm_ts_summary": (_i32, [_p, _i64, _i64, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
+                             _p, _p]),
+    "fm_rolling_mean": (_i32, [_p, _i64, _i64, _p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p]),
+    "fm_predictive": (_i32, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p,
+                             _p]),
+    "fm_forecast": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p]),
+    "fm_gen_panel": (_i32, [C.c_uint64, _i64, _i32, _i32, _f64, _f64, _p, _i64, _p, _p, _p]),
+    "fm_stream_probe": (_i32, [_p, _i64, _p, _p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+class FMError(RuntimeError):
+    """A libfm_hip entry point returned an error code."""
+
+
+def load():
+    """Load libfm_hip.so (once).  Raises ImportError if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libfm_hip.so not found at {LIB_PATH}; build it with "
+            "`make -C fm-returnprediction_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.fm_last_error().decode(errors="replace")
+        raise FMError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def version():
+    return load().fm_version().decode()

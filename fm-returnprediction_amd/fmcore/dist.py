@@ -1,0 +1,63 @@
+"""Month sharding across GPUs (one process per GPU, torch.distributed over RCCL/xGMI).
+
+Every panel-sized step is independent per month (cuts, universes, Gram, solve), so each
+rank owns a contiguous month range, balanced by row count, and never exchanges panel rows.
+The only exchanges:
+  1. all-gather of the per-(month, problem) records {intercept, slopes, R2, N} and status
+     (a few KB per month) before the time-series stage, which every rank then runs on the
+     full series (FM means, Newey-West, 120-month rolling windows: no halos needed);
+  2. a sum all-reduce of the predictive-slope records, each rank having filled the rows of
+     its own months from its local centered moments.
+The helpers are device-agnostic so the same code runs under gloo on CPU in the tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(seg_rows, world):
+    """Contiguous month ranges [s0, s1) per rank, balanced by cumulative row count."""
+    seg_rows = np.asarray(seg_rows, dtype=np.int64)
+    T = len(seg_rows)
+    cum = np.concatenate([[0], np.cumsum(seg_rows)])
+    total = cum[-1]
+    bounds = [0]
+    for r in range(1, world):
+        target = total * r / world
+        s = int(np.searchsorted(cum, target, side="left"))
+        s = min(max(s, bounds[-1]), T)
+        bounds.append(s)
+    bounds.append(T)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def _gather_rows(t, counts, group=None):
+    """All-gather a [T_local, ...] tensor whose first dim differs per rank."""
+    world = dist.get_world_size(group)
+    tmax = max(counts)
+    pad = torch.zeros((tmax,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat([parts[r][: counts[r]] for r in range(world)], dim=0)
+
+
+def gather_records(rec, status, counts, group=None):
+    """Global [T, P, rs] records and [T, P] status from each rank's local months."""
+    return _gather_rows(rec, counts, group), _gather_rows(status, counts, group)
+
+
+def combine_predictive(pred, pst, group=None):
+    """Rows of other ranks' months are zero in `pred`/`pst`: a SUM all-reduce merges them
+    (each compact row has exactly one owner)."""
+    dist.all_reduce(pred, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(pst, op=dist.ReduceOp.SUM, group=group)
+    return pred, pst
+
+
+def max_over_ranks(x, device, group=None):
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

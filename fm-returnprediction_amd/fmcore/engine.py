@@ -1,0 +1,555 @@
+"""Device-resident Fama-MacBeth engine: host orchestration of libfm_hip kernels.
+
+torch (ROCm) only provides device buffers and the stream; every computation on the hot
+path is a libfm_hip kernel.  There is no CPU fallback: without a HIP device the
+functions raise.
+
+Layout in HBM (``DevicePanel``): one FP64 SoA block ``cols[C, n]`` with rows sorted by
+(month, input order) — month segments are CSR ``seg_off[T+1]`` — plus optional ``me``
+(FP64) and ``nyse`` (uint8) rows and a uint8 universe ``level`` per row.
+"""
+from __future__ import annotations
+
+import itertools
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+# statsmodels/numpy quantile modes
+LERP_NUMPY = 0
+LERP_PANDAS = 1
+
+
+def require_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("fmcore needs a HIP device (MI355X); none is visible and there is "
+                           "no CPU fallback")
+    L.load()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class KernelTimer:
+    """Records HIP events on the current stream around every libfm_hip launch made by
+    this module while active (bench.py uses it for the per-kernel roofline)."""
+
+    def __init__(self):
+        self.events = {}
+
+    def __enter__(self):
+        global _TIMER
+        _TIMER = self
+        return self
+
+    def __exit__(self, *exc):
+        global _TIMER
+        _TIMER = None
+
+    def avg_ms(self, name):
+        torch.cuda.synchronize()
+        ev = self.events.get(name, [])
+        if not ev:
+            return float("nan")
+        return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    def names(self):
+        return list(self.events)
+
+
+_TIMER = None
+
+
+def _kcall(tag, name, *args):
+    t = _TIMER
+    if t is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    L.call(name, *args)
+    if t is not None:
+        e1.record()
+        t.events.setdefault(tag, []).append((e0, e1))
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ------------------------------------------------------------------------------------------
+# Panel
+# ------------------------------------------------------------------------------------------
+@dataclass
+class DevicePanel:
+    cols: torch.Tensor                 # [C, n] float64, contiguous
+    names: List[str]
+    seg_off: torch.Tensor              # [T+1] int64 (device)
+    seg_off_h: np.ndarray              # [T+1] int64 (host)
+    months: object = None              # segment labels (host)
+    me: Optional[torch.Tensor] = None  # [n] float64
+    nyse: Optional[torch.Tensor] = None  # [n] uint8
+    order: Optional[np.ndarray] = None   # sorted row -> original positional row
+
+    @property
+    def nrows(self):
+        return int(self.seg_off_h[-1])
+
+    @property
+    def nseg(self):
+        return len(self.seg_off_h) - 1
+
+    @property
+    def ncols(self):
+        return self.cols.shape[0]
+
+    @property
+    def stride(self):
+        return self.cols.stride(0)
+
+    @property
+    def max_seg_len(self):
+        return int(np.diff(self.seg_off_h).max()) if self.nseg else 0
+
+    def col(self, name):
+        return self.names.index(name)
+
+
+def month_segments(labels):
+    """Factorize month labels (sorted) -> (codes, uniques, stable order of valid rows,
+    seg_off).  Rows with a missing label are excluded (pandas groupby/dropna drop them)."""
+    import pandas as pd
+    codes, uniq = pd.factorize(labels, sort=True)
+    codes = np.asarray(codes)
+    order = np.argsort(codes, kind="stable")
+    order = order[codes[order] >= 0]
+    counts = np.bincount(codes[codes >= 0], minlength=len(uniq))
+    seg_off = np.zeros(len(uniq) + 1, dtype=np.int64)
+    np.cumsum(counts, out=seg_off[1:])
+    return codes, uniq, order, seg_off
+
+
+def panel_from_arrays(arrays: Sequence[np.ndarray], names, labels, me=None, nyse=None,
+                      device=None):
+    """Upload host columns (original row order) and permute them month-major on device."""
+    device = device or require_device()
+    _, uniq, order, seg_off = month_segments(labels)
+    n_in = len(labels)
+    host = np.empty((len(arrays), n_in), dtype=np.float64)
+    for i, a in enumerate(arrays):
+        host[i] = np.asarray(a, dtype=np.float64)
+    raw = torch.from_numpy(host).to(device, non_blocking=False)
+    perm = torch.from_numpy(order.astype(np.int64)).to(device)
+    cols = raw.index_select(1, perm).contiguous()
+    me_t = nyse_t = None
+    if me is not None:
+        me_t = torch.from_numpy(np.asarray(me, dtype=np.float64)).to(device).index_select(0, perm)
+    if nyse is not None:
+        nyse_t = torch.from_numpy(np.asarray(nyse, dtype=np.uint8)).to(device).index_select(0, perm)
+    return DevicePanel(cols=cols, names=list(names), seg_off=torch.from_numpy(seg_off).to(device),
+                       seg_off_h=seg_off, months=uniq, me=me_t, nyse=nyse_t, order=order)
+
+
+def panel_synthetic(nmonths, nfirms, seed, month0=0, nan_rate=0.02, nyse_rate=0.4, device=None):
+    """Generate a balanced synthetic panel directly in HBM (fm_gen_panel; identical to
+    fmcore.synth.synth_arrays with present_rate=1)."""
+    from .synth import WINSOR_VARS
+    device = device or require_device()
+    n = nmonths * nfirms
+    cols = torch.empty((len(WINSOR_VARS), n), dtype=torch.float64, device=device)
+    me = torch.empty(n, dtype=torch.float64, device=device)
+    nyse = torch.empty(n, dtype=torch.uint8, device=device)
+    _kcall("fm_gen_panel", "fm_gen_panel", seed, month0, nmonths, nfirms, nan_rate, nyse_rate, cols.data_ptr(),
+           cols.stride(0), me.data_ptr(), nyse.data_ptr(), _stream())
+    seg_off = np.arange(nmonths + 1, dtype=np.int64) * nfirms
+    return DevicePanel(cols=cols, names=list(WINSOR_VARS), seg_off=torch.from_numpy(seg_off).to(device),
+                       seg_off_h=seg_off, months=np.arange(month0, month0 + nmonths), me=me, nyse=nyse)
+
+
+# ------------------------------------------------------------------------------------------
+# Order statistics, clipping, universes
+# ------------------------------------------------------------------------------------------
+@dataclass
+class Cuts:
+    lo: torch.Tensor      # [C, T]
+    hi: torch.Tensor
+    nvalid: torch.Tensor  # [C, T] int32
+    mean: Optional[torch.Tensor] = None
+    sd: Optional[torch.Tensor] = None
+
+
+def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols=None,
+                row_mask=None, moments=False, tag="fm_select_cuts"):
+    """Per (column, month) quantile cuts.  ``cols`` defaults to panel.cols."""
+    src = panel.cols if cols is None else cols
+    if src.dim() == 1:
+        src = src.view(1, -1)
+    C, T = src.shape[0], panel.nseg
+    dev = src.device
+    lo = torch.empty((C, T), dtype=torch.float64, device=dev)
+    hi = torch.empty_like(lo)
+    nv = torch.empty((C, T), dtype=torch.int32, device=dev)
+    mean = sd = None
+    if moments:
+        mean = torch.empty_like(lo)
+        sd = torch.empty_like(lo)
+    _kcall(tag, "fm_select_cuts", src.data_ptr(), src.stride(0), C, panel.seg_off.data_ptr(), T,
+           max(panel.max_seg_len, 1), _ptr(row_mask), float(q_lo), float(q_hi), int(min_count),
+           int(mode), lo.data_ptr(), hi.data_ptr(), nv.data_ptr(), _ptr(mean), _ptr(sd), _stream())
+    return Cuts(lo, hi, nv, mean, sd)
+
+
+def clip(panel: DevicePanel, cuts: Cuts, out=None):
+    out = torch.empty_like(panel.cols) if out is None else out
+    _kcall("fm_clip", "fm_clip", panel.cols.data_ptr(), out.data_ptr(), panel.stride, panel.ncols,
+           panel.seg_off.data_ptr(), panel.nseg, panel.nrows, cuts.lo.data_ptr(), cuts.hi.data_ptr(),
+           _stream())
+    return out
+
+
+def standardize(panel: DevicePanel, mean, sd, src=None, out=None):
+    src = panel.cols if src is None else src
+    out = torch.empty_like(src) if out is None else out
+    _kcall("fm_standardize", "fm_standardize", src.data_ptr(), out.data_ptr(), src.stride(0), src.shape[0],
+           panel.seg_off.data_ptr(), panel.nseg, panel.nrows, mean.data_ptr(), sd.data_ptr(),
+           _stream())
+    return out
+
+
+def nyse_breakpoints(panel: DevicePanel, q_a=0.2, q_b=0.5):
+    """me_20 / me_50 per month over NYSE rows (pandas groupby.quantile lerp)."""
+    cuts = select_cuts(panel, q_a, q_b, 1, LERP_PANDAS, cols=panel.me.view(1, -1), row_mask=panel.nyse,
+                       tag="fm_select_cuts[nyse]")
+    return cuts.lo[0], cuts.hi[0]
+
+
+def universe_level(panel: DevicePanel, cut_a, cut_b):
+    level = torch.empty(panel.nrows, dtype=torch.uint8, device=panel.cols.device)
+    _kcall("fm_universe_level", "fm_universe_level", panel.me.data_ptr(), panel.seg_off.data_ptr(), panel.nseg,
+           panel.nrows, cut_a.data_ptr(), cut_b.data_ptr(), level.data_ptr(), _stream())
+    return level
+
+
+def pilot_shift(panel: DevicePanel, cols=None):
+    src = panel.cols if cols is None else cols
+    sh = torch.empty((src.shape[0], panel.nseg), dtype=torch.float64, device=src.device)
+    _kcall("fm_pilot_shift", "fm_pilot_shift", src.data_ptr(), src.stride(0), src.shape[0], panel.seg_off.data_ptr(),
+           panel.nseg, sh.data_ptr(), _stream())
+    return sh
+
+
+# ------------------------------------------------------------------------------------------
+# Models, problems, the batched Gram pass
+# ------------------------------------------------------------------------------------------
+@dataclass
+class Model:
+    name: str
+    y: int                       # panel column of the dependent variable
+    xs: List[int]                # panel columns of the regressors (order = output order)
+    levels: Sequence[int] = (0,)  # universe levels to solve (0 all, 1 all-but-tiny, 2 large)
+    const_check: bool = True     # add_constant(has_constant='skip') semantics (regressions.py)
+
+    @property
+    def mask(self):
+        m = 1 << self.y
+        for x in self.xs:
+            m |= 1 << x
+        return m
+
+
+@dataclass
+class Problem:
+    model: int
+    level: int
+    K: int
+
+
+@dataclass
+class FMResult:
+    problems: List[Problem]
+    rec: torch.Tensor            # [T, nprob, pmax+2]
+    status: torch.Tensor         # [T, nprob] int32 (FM_ST_* bits)
+    pmax: int
+    moments: Optional[torch.Tensor] = None   # [T, nprob, mom_stride]
+    mom_stride: int = 0
+
+    @property
+    def nprob(self):
+        return len(self.problems)
+
+
+def plan_patterns(models: Sequence[Model]):
+    """Validity patterns that can occur: if model a's columns are a subset of model b's,
+    every row valid for b is valid for a.  Returns (lut[1<<M] uint8, pattern_models)."""
+    M = len(models)
+    masks = [m.mask for m in models]
+    pats = []
+    for P in range(1, 1 << M):
+        ok = True
+        for a, b in itertools.permutations(range(M), 2):
+            if (masks[a] & masks[b]) == masks[a] and (P >> b) & 1 and not (P >> a) & 1:
+                ok = False
+                break
+        if ok:
+            pats.append(P)
+    lut = np.full(1 << M, 255, dtype=np.uint8)
+    for i, P in enumerate(pats):
+        lut[P] = i
+    return lut, pats
+
+
+def group_models(models: Sequence[Model], nlevels, cap):
+    """Split models into groups whose bucket count (patterns x levels) fits ``cap``."""
+    groups, cur = [], []
+    for i, m in enumerate(models):
+        trial = cur + [i]
+        if len(trial) > L.FM_MAX_MODELS or len(plan_patterns([models[j] for j in trial])[1]) * nlevels > cap:
+            if not cur:
+                raise ValueError("a single model exceeds the bucket budget")
+            groups.append(cur)
+            cur = [i]
+        else:
+            cur = trial
+    if cur:
+        groups.append(cur)
+    return groups
+
+
+def make_chunks(seg_off_h, target_chunks=2048, min_rows=512):
+    n = int(seg_off_h[-1])
+    T = len(seg_off_h) - 1
+    ch = max(min_rows, -(-n // max(target_chunks, 1)))
+    ch = ((ch + 255) // 256) * 256
+    lens = np.diff(seg_off_h)
+    nch = np.maximum(1, -(-lens // ch)).astype(np.int64)
+    seg = np.repeat(np.arange(T, dtype=np.int32), nch)
+    k = np.arange(len(seg)) - np.repeat(np.cumsum(nch) - nch, nch)
+    r0 = seg_off_h[seg] + k * ch
+    r1 = np.minimum(r0 + ch, seg_off_h[seg + 1])
+    rows = np.stack([r0, r1], axis=1).reshape(-1).astype(np.int64)
+    off = np.zeros(T + 1, dtype=np.int32)
+    np.cumsum(nch, out=off[1:])
+    return seg, rows, off
+
+
+@dataclass
+class _Plan:
+    chunk_seg: torch.Tensor
+    chunk_row: torch.Tensor
+    seg_chunk_off: torch.Tensor
+    nchunks: int
+
+
+def _chunk_plan(panel: DevicePanel):
+    cache = getattr(panel, "_chunk_cache", None)
+    if cache is not None:
+        return cache
+    seg, rows, off = make_chunks(panel.seg_off_h)
+    dev = panel.cols.device
+    plan = _Plan(torch.from_numpy(seg).to(dev), torch.from_numpy(rows).to(dev),
+                 torch.from_numpy(off).to(dev), len(seg))
+    panel._chunk_cache = plan
+    return plan
+
+
+def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, cuts: Cuts = None,
+            shift=None, inv_scale=None, add_back=None, moments=False, cols=None, const_check=True):
+    """One batched cross-sectional pass: every (model, universe level) problem for every
+    month from one read of the panel per model group.  Returns an FMResult."""
+    src = panel.cols if cols is None else cols
+    ncols = src.shape[0]
+    if ncols > L.FM_MAX_COLS:
+        raise ValueError(f"at most {L.FM_MAX_COLS} columns per pass")
+    dev = src.device
+    T = panel.nseg
+    zw = 16 if ncols <= 15 else 32
+    cap = 16 if zw == 16 else 8
+    if shift is None:
+        shift = pilot_shift(panel, src)
+    if add_back is None and inv_scale is None:
+        add_back = shift
+    problems = []
+    for mi, m in enumerate(models):
+        for u in m.levels:
+            if u >= nlevels:
+                raise ValueError("model level beyond the universe levels provided")
+            problems.append(Problem(mi, u, len(m.xs)))
+    pmax = max(2, max(p.K + 1 for p in problems))
+    nprob = len(problems)
+    rs = pmax + 2
+    rec = torch.empty((T, nprob, rs), dtype=torch.float64, device=dev)
+    status = torch.zeros((T, nprob), dtype=torch.int32, device=dev)
+    mom_stride = 1 + (pmax + 1) + (pmax + 1) ** 2
+    mom = torch.empty((T, nprob, mom_stride), dtype=torch.float64, device=dev) if moments else None
+    plan = _chunk_plan(panel)
+    lo = cuts.lo if cuts is not None else None
+    hi = cuts.hi if cuts is not None else None
+    groups = group_models(models, nlevels, cap)
+    for g in groups:
+        gm = [models[i] for i in g]
+        lut, pats = plan_patterns(gm)
+        nb = len(pats) * nlevels
+        mm = torch.tensor([m.mask for m in gm], dtype=torch.int64).to(torch.int32).to(dev)
+        ym = torch.tensor([1 << m.y for m in gm], dtype=torch.int32, device=dev)
+        lut_t = torch.from_numpy(lut).to(dev)
+        partial = torch.empty((plan.nchunks, nb, zw * zw), dtype=torch.float64, device=dev)
+        flags = torch.zeros((T, len(gm)), dtype=torch.int32, device=dev)
+        ga = L.GramArgs(
+            cols=src.data_ptr(), col_stride=src.stride(0), ncols=ncols, nseg=T,
+            seg_off=panel.seg_off.data_ptr(), chunk_seg=plan.chunk_seg.data_ptr(),
+            chunk_row=plan.chunk_row.data_ptr(), nchunks=plan.nchunks,
+            lo=_ptr(lo), hi=_ptr(hi), shift=_ptr(shift), inv_scale=_ptr(inv_scale),
+            level=_ptr(level), nlevels=nlevels, model_mask=mm.data_ptr(), model_ymask=ym.data_ptr(),
+            nmodels=len(gm), pattern_id=lut_t.data_ptr(), npatterns=len(pats),
+            partial=partial.data_ptr(), flags=flags.data_ptr())
+        _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
+        gp = [(k, p) for k, p in enumerate(problems) if p.model in g]
+        local = {mi: j for j, mi in enumerate(g)}
+        pz = np.zeros((len(gp), 32), dtype=np.int32)
+        pnz = np.zeros(len(gp), dtype=np.int32)
+        for j, (_, p) in enumerate(gp):
+            m = models[p.model]
+            z = [0] + [1 + x for x in m.xs] + [1 + m.y]
+            pz[j, :len(z)] = z
+            pnz[j] = len(z)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        pm = t(np.array([local[p.model] for _, p in gp], dtype=np.int32))
+        pl = t(np.array([p.level for _, p in gp], dtype=np.int32))
+        pf = t(np.array([1 if (models[p.model].const_check and const_check) else 0 for _, p in gp],
+                        dtype=np.int32))
+        pzt, pnzt = t(pz), t(pnz)
+        patm = t(np.array(pats, dtype=np.int64).astype(np.uint32).view(np.int32))
+        grec = torch.empty((T, len(gp), rs), dtype=torch.float64, device=dev)
+        gst = torch.zeros((T, len(gp)), dtype=torch.int32, device=dev)
+        gmom = torch.empty((T, len(gp), mom_stride), dtype=torch.float64, device=dev) if moments else None
+        sa = L.SolveArgs(
+            partial=partial.data_ptr(), seg_chunk_off=plan.seg_chunk_off.data_ptr(), nseg=T, zw=zw,
+            nlevels=nlevels, npatterns=len(pats), pattern_models=patm.data_ptr(), nprob=len(gp),
+            prob_model=pm.data_ptr(), prob_level=pl.data_ptr(), prob_z=pzt.data_ptr(),
+            prob_nz=pnzt.data_ptr(), prob_flags=pf.data_ptr(), add_back=_ptr(add_back),
+            gram_flags=flags.data_ptr(), nmodels=len(gm), pmax=pmax, rec=grec.data_ptr(),
+            status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride)
+        _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
+        idx = torch.tensor([k for k, _ in gp], dtype=torch.int64, device=dev)
+        if len(groups) == 1:
+            rec, status, mom = grec, gst, gmom
+        else:
+            rec.index_copy_(1, idx, grec)
+            status.index_copy_(1, idx, gst)
+            if moments:
+                mom.index_copy_(1, idx, gmom)
+        # exact nonzero-constant test where the Gram flagged a near-zero variance
+        if const_check:
+            sus = ((gst & L.FM_ST_CONST_SUSPECT) != 0).nonzero()
+            if sus.numel():
+                pairs = sus.to(torch.int32).contiguous()
+                _kcall("fm_const_check", "fm_const_check", src.data_ptr(), src.stride(0), ncols, panel.seg_off.data_ptr(),
+                       T, _ptr(lo), _ptr(hi), _ptr(level), len(gp), pl.data_ptr(), pzt.data_ptr(),
+                       pnzt.data_ptr(), pairs.data_ptr(), pairs.shape[0], gst.data_ptr(), _stream())
+                if len(groups) == 1:
+                    status = gst
+                else:
+                    status.index_copy_(1, idx, gst)
+    return FMResult(problems=problems, rec=rec, status=status, pmax=pmax, moments=mom,
+                    mom_stride=mom_stride)
+
+
+# ------------------------------------------------------------------------------------------
+# Time-series stage
+# ------------------------------------------------------------------------------------------
+@dataclass
+class TSIndex:
+    idx: torch.Tensor     # [nprob, T] int32: fitted months in order
+    count: torch.Tensor   # [nprob] int32
+
+
+def ts_compact(status, s_seg, s_prob, nseg, nprob):
+    dev = status.device
+    idx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
+    cnt = torch.empty(nprob, dtype=torch.int32, device=dev)
+    _kcall("fm_ts_compact", "fm_ts_compact", status.data_ptr(), s_seg, s_prob, nseg, nprob, idx.data_ptr(),
+           cnt.data_ptr(), _stream())
+    return TSIndex(idx, cnt)
+
+
+def compact_result(res: FMResult):
+    T, P = res.status.shape
+    return ts_compact(res.status, P, 1, T, P)
+
+
+@dataclass
+class Summary:
+    mean: torch.Tensor   # [nprob, kmax]
+    se: torch.Tensor
+    tstat: torch.Tensor
+    nobs: torch.Tensor
+
+
+def ts_summary(rec, r_seg, r_prob, ix: TSIndex, nseg, nprob, kmax, nw_lags=4):
+    dev = rec.device
+    mean = torch.empty((nprob, kmax), dtype=torch.float64, device=dev)
+    se, ts = torch.empty_like(mean), torch.empty_like(mean)
+    nobs = torch.empty((nprob, kmax), dtype=torch.int32, device=dev)
+    work = torch.empty((nprob, kmax, max(nseg, 1)), dtype=torch.float64, device=dev)
+    _kcall("fm_ts_summary", "fm_ts_summary", rec.data_ptr(), r_seg, r_prob, ix.idx.data_ptr(), ix.count.data_ptr(),
+           nseg, nprob, kmax, nw_lags, mean.data_ptr(), se.data_ptr(), ts.data_ptr(), nobs.data_ptr(),
+           work.data_ptr(), _stream())
+    return Summary(mean, se, ts, nobs)
+
+
+def summarize_result(res: FMResult, ix: TSIndex = None, nw_lags=4):
+    ix = ix or compact_result(res)
+    T, P, rs = res.rec.shape
+    return ts_summary(res.rec, P * rs, rs, ix, T, P, rs, nw_lags), ix
+
+
+def rolling_result(res: FMResult, ix: TSIndex, window=120, min_periods=60):
+    T, P, rs = res.rec.shape
+    out = torch.empty((P, T, res.pmax), dtype=torch.float64, device=res.rec.device)
+    _kcall("fm_rolling_mean", "fm_rolling_mean", res.rec.data_ptr(), P * rs, rs, ix.idx.data_ptr(), ix.count.data_ptr(),
+           T, P, res.pmax, window, min_periods, out.data_ptr(), _stream())
+    return out
+
+
+def predictive_result(res: FMResult, ix: TSIndex, roll, lag=1, seg_lo=0, seg_hi=None, moments=None):
+    """A7/A8 per (problem, fitted-month row): slope, R2, N of y on the lagged-rolling
+    forecast, from the month's centered moments.  In sharded runs ``res`` holds the
+    gathered global records and ``moments`` the local months [seg_lo, seg_hi) only."""
+    T, P, _ = res.rec.shape
+    dev = res.rec.device
+    mom = res.moments if moments is None else moments
+    seg_hi = T if seg_hi is None else seg_hi
+    pk = torch.tensor([p.K for p in res.problems], dtype=torch.int32, device=dev)
+    pred = torch.empty((P, T, 4), dtype=torch.float64, device=dev)
+    pst = torch.empty((P, T), dtype=torch.int32, device=dev)
+    _kcall("fm_predictive", "fm_predictive", mom.data_ptr(), res.mom_stride, T, P, pk.data_ptr(),
+           ix.idx.data_ptr(), ix.count.data_ptr(), roll.data_ptr(), res.pmax, lag, seg_lo, seg_hi,
+           pred.data_ptr(), pst.data_ptr(), _stream())
+    return pred, pst
+
+
+def summarize_predictive(pred, pst, nw_lags=4):
+    P, T, _ = pred.shape
+    ix = ts_compact(pst, 1, T, T, P)
+    return ts_summary(pred, 4, T * 4, ix, T, P, 3, nw_lags), ix
+
+
+def forecast(panel: DevicePanel, coef, cols=None):
+    """A7 per-row forecasts F = c0[t] + sum_k c_k[t] x_k for coef [T, K+1] (NaN propagates)."""
+    src = panel.cols if cols is None else cols
+    coef = coef.contiguous()
+    out = torch.empty(panel.nrows, dtype=torch.float64, device=src.device)
+    _kcall("fm_forecast", "fm_forecast", src.data_ptr(), src.stride(0), src.shape[0], panel.seg_off.data_ptr(),
+           panel.nseg, panel.nrows, coef.data_ptr(), coef.stride(0), out.data_ptr(), _stream())
+    return out
+
+
+def stream_probe(t):
+    out = torch.zeros(1, dtype=torch.float64, device=t.device)
+    _kcall("fm_stream_probe", "fm_stream_probe", t.data_ptr(), t.numel(), out.data_ptr(), _stream())
+    return out

@@ -1,0 +1,183 @@
+/*
+ * fm_hip.h — C ABI of libfm_hip.so, the MI355X (gfx950) Fama-MacBeth engine.
+ *
+ * Drop-in boundary.  The reference (BaileyMeche/FM-ReturnPrediction) has no FFI layer: its
+ * hot path is a set of pandas-in/pandas-out Python functions.  The Python mirror in
+ * fm-returnprediction_amd/src/{regressions,calc_Lewellen_2014}.py keeps those names and
+ * signatures and calls the entry points below through ctypes.  Each entry point names
+ * the reference computation it replaces:
+ *
+ *   fm_select_cuts  <- np.percentile(vals, 1/99) per month per var
+ *                      (src/calc_Lewellen_2014.py:519-523) and pandas
+ *                      groupby("mthcaldt")["me"].quantile([.2,.5]) over NYSE rows (:74-82)
+ *   fm_clip         <- subdf[var].clip(lower, upper) (src/calc_Lewellen_2014.py:524)
+ *   fm_standardize  <- per-month z-score (north-star extension; no reference line)
+ *   fm_universe_level <- me >= me_20 / me >= me_50 masks (src/calc_Lewellen_2014.py:95-96)
+ *   fm_pilot_shift  <- (numerics only) per-month pivot used to center the Gram
+ *   fm_gram         <- dropna (src/regressions.py:39) + X'X, X'y, y'y inside sm.OLS
+ *                      (src/regressions.py:57; src/calc_Lewellen_2014.py:917-919), batched
+ *                      over models x universes in one read of the panel
+ *   fm_solve        <- sm.OLS(Y, X).fit() params / rsquared / N and the N<K+1 skip
+ *                      (src/regressions.py:52-72; src/calc_Lewellen_2014.py:914-921)
+ *   fm_const_check  <- add_constant(has_constant='skip') nonzero-constant detection
+ *                      (src/regressions.py:50, which leads to IndexError at :71)
+ *   fm_ts_compact, fm_ts_summary <- fama_macbeth_summary + newey_west_mean_se
+ *                      (src/regressions.py:78-131)
+ *   fm_rolling_mean <- slopes_df.rolling(window=120, min_periods=60).mean()
+ *                      (src/calc_Lewellen_2014.py:926)
+ *   fm_predictive   <- build-defined extension: lagged-rolling-coefficient forecasts and
+ *                      predictive-slope regressions (paper Table 3; no reference line)
+ *   fm_forecast     <- build-defined extension A7: per-row F = a_{t-1} + b_{t-1}'x_t
+ *   fm_gen_panel    <- (bench/test data) counter-based synthetic panel, bit-identical to
+ *                      fmcore/synth.py
+ *
+ * Conventions: every pointer is device memory allocated by the caller (PyTorch); the
+ * library never allocates device memory and keeps no pointer after return.  `stream` is a
+ * hipStream_t passed as void*; all work is enqueued on it asynchronously.  Return 0 on
+ * success, < 0 on error (fm_last_error() has the message, per thread).  Panels are
+ * column-major SoA: column c of a panel is cols[c*col_stride + row], rows sorted by
+ * (month, permno); seg_off[nseg+1] are the month (segment) row offsets.
+ */
+#ifndef FM_HIP_H
+#define FM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FM_OK 0
+#define FM_EINVAL (-1)
+#define FM_EHIP (-2)
+#define FM_ETOOBIG (-3)
+
+/* per (segment, problem) status bits */
+#define FM_ST_FITTED 0x1u
+#define FM_ST_SKIPPED 0x2u        /* N < K+1: month absent from the output            */
+#define FM_ST_INF_IN_X 0x4u       /* statsmodels MissingDataError('exog contains inf') */
+#define FM_ST_INF_IN_Y 0x8u
+#define FM_ST_CONST_SUSPECT 0x10u /* near-zero centered variance; exact check pending  */
+#define FM_ST_CONST_COL 0x20u     /* nonzero constant regressor -> IndexError          */
+#define FM_ST_RANK_DEF 0x40u      /* pinv fallback (Jacobi eigen) used                 */
+
+#define FM_MAX_COLS 31            /* z = [1, cols] fits two 16-wide MFMA tiles          */
+#define FM_MAX_MODELS 6
+#define FM_MAX_LEVELS 3
+
+typedef struct fm_gram_args {
+    const double* cols;       /* [ncols][col_stride] */
+    int64_t col_stride;
+    int32_t ncols;            /* <= FM_MAX_COLS */
+    int32_t nseg;
+    const int64_t* seg_off;   /* [nseg+1] */
+    const int32_t* chunk_seg; /* [nchunks] segment of each chunk */
+    const int64_t* chunk_row; /* [2*nchunks]: (row0, row1) of each chunk, inside one segment */
+    int32_t nchunks;
+    const double* lo;         /* [ncols][nseg] clip bounds or NULL (NaN bound = none) */
+    const double* hi;
+    const double* shift;      /* [ncols][nseg] pivot subtracted before accumulation, or NULL */
+    const double* inv_scale;  /* [ncols][nseg] multiplier after the shift (standardize), or NULL */
+    const uint8_t* level;     /* [rows] universe level 0..nlevels-1, or NULL */
+    int32_t nlevels;
+    const uint32_t* model_mask;   /* [nmodels] bit c: column c must be non-NaN */
+    const uint32_t* model_ymask;  /* [nmodels] bit of the dependent column */
+    int32_t nmodels;
+    const uint8_t* pattern_id;    /* [1<<nmodels] validity pattern -> id, 255 = drop row */
+    int32_t npatterns;            /* buckets = npatterns * nlevels */
+    double* partial;              /* [nchunks][nbuckets][zw*zw], zw = 16 or 32 */
+    uint32_t* flags;              /* [nseg][nmodels], OR-ed FM_ST_INF_IN_X / _Y; zeroed by caller */
+} fm_gram_args;
+
+typedef struct fm_solve_args {
+    const double* partial;        /* from fm_gram */
+    const int32_t* seg_chunk_off; /* [nseg+1] chunk range of each segment */
+    int32_t nseg;
+    int32_t zw;                   /* 16 or 32 */
+    int32_t nlevels;
+    int32_t npatterns;
+    const uint32_t* pattern_models; /* [npatterns] bitmask of models valid in that pattern */
+    int32_t nprob;
+    const int32_t* prob_model;    /* [nprob] */
+    const int32_t* prob_level;    /* [nprob] universe level u: buckets with level >= u */
+    const int32_t* prob_z;        /* [nprob][32] z indices: 0 (intercept), x..., y */
+    const int32_t* prob_nz;       /* [nprob] number of z indices P+1 (<= 32) */
+    const int32_t* prob_flags;    /* [nprob] bit0: check nonzero-constant columns */
+    const double* add_back;       /* [ncols][nseg] shift to add back for raw intercept, or NULL */
+    const uint32_t* gram_flags;   /* [nseg][nmodels] from fm_gram, or NULL */
+    int32_t nmodels;
+    int32_t pmax;                 /* >= max P (= K+1) over problems, <= 32 */
+    double* rec;                  /* [nseg][nprob][pmax+2]: intercept, slopes..., NaN pad,
+                                     R2 at [pmax], N at [pmax+1] */
+    uint32_t* status;             /* [nseg][nprob] FM_ST_* bits */
+    double* moments;              /* [nseg][nprob][mom_stride] or NULL: n, means(K+1), centered (K+1)^2 */
+    int32_t mom_stride;
+} fm_solve_args;
+
+const char* fm_version(void);
+const char* fm_last_error(void);
+int fm_abi_sizes(int32_t* gram_args, int32_t* solve_args);
+int fm_device_arch(char* buf, int32_t len);
+
+int fm_select_cuts(const double* cols, int64_t col_stride, int32_t ncols,
+                   const int64_t* seg_off, int32_t nseg, int32_t max_seg_len,
+                   const uint8_t* row_mask, double q_lo, double q_hi, int32_t min_count,
+                   int32_t lerp_mode, double* lo, double* hi, int32_t* nvalid,
+                   double* mean, double* sd, void* stream);
+
+int fm_clip(const double* src, double* dst, int64_t col_stride, int32_t ncols,
+            const int64_t* seg_off, int32_t nseg, int64_t nrows,
+            const double* lo, const double* hi, void* stream);
+
+int fm_standardize(const double* src, double* dst, int64_t col_stride, int32_t ncols,
+                   const int64_t* seg_off, int32_t nseg, int64_t nrows,
+                   const double* mean, const double* sd, void* stream);
+
+int fm_universe_level(const double* me, const int64_t* seg_off, int32_t nseg, int64_t nrows,
+                      const double* cut_a, const double* cut_b, uint8_t* level, void* stream);
+
+int fm_pilot_shift(const double* cols, int64_t col_stride, int32_t ncols,
+                   const int64_t* seg_off, int32_t nseg, double* shift, void* stream);
+
+int fm_gram(const fm_gram_args* args, void* stream);
+
+int fm_solve(const fm_solve_args* args, void* stream);
+
+int fm_const_check(const double* cols, int64_t col_stride, int32_t ncols,
+                   const int64_t* seg_off, int32_t nseg,
+                   const double* lo, const double* hi, const uint8_t* level,
+                   int32_t nprob, const int32_t* prob_level, const int32_t* prob_z,
+                   const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
+                   uint32_t* status, void* stream);
+
+int fm_ts_compact(const uint32_t* status, int64_t s_seg, int64_t s_prob, int32_t nseg,
+                  int32_t nprob, int32_t* idx, int32_t* count, void* stream);
+
+int fm_ts_summary(const double* rec, int64_t r_seg, int64_t r_prob, const int32_t* idx,
+                  const int32_t* count, int32_t nseg, int32_t nprob, int32_t kmax,
+                  int32_t nw_lags, double* mean, double* se, double* tstat, int32_t* nobs,
+                  double* work, void* stream);
+
+int fm_rolling_mean(const double* rec, int64_t r_seg, int64_t r_prob, const int32_t* idx,
+                    const int32_t* count, int32_t nseg, int32_t nprob, int32_t kmax,
+                    int32_t window, int32_t min_periods, double* out, void* stream);
+
+int fm_predictive(const double* moments, int32_t mom_stride, int32_t nseg, int32_t nprob,
+                  const int32_t* prob_k, const int32_t* idx, const int32_t* count,
+                  const double* rolling, int32_t pmax, int32_t lag, int32_t seg_lo,
+                  int32_t seg_hi, double* pred, uint32_t* pred_status, void* stream);
+
+int fm_forecast(const double* cols, int64_t col_stride, int32_t K, const int64_t* seg_off,
+                int32_t nseg, int64_t nrows, const double* coef, int32_t coef_stride,
+                double* out, void* stream);
+
+int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
+                 double nan_rate, double nyse_rate, double* cols, int64_t col_stride,
+                 double* me, uint8_t* nyse, void* stream);
+
+int fm_stream_probe(const double* src, int64_t n, double* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
