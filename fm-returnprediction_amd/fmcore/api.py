@@ -28,7 +28,8 @@ def raise_like_reference(status, K, what="exog"):
     nonzero-constant regressor add_constant skips the intercept and the slope loop raises
     IndexError (reference src/regressions.py:50,57,71)."""
     st = np.asarray(status)
-    bad = np.nonzero((st & L.FM_ST_FITTED) & ((st & L.FM_ST_INF_IN_X) | (st & L.FM_ST_CONST_COL)))[0]
+    bad = np.nonzero(((st & L.FM_ST_FITTED) != 0) &
+                     ((st & (L.FM_ST_INF_IN_X | L.FM_ST_CONST_COL)) != 0))[0]
     if bad.size == 0:
         return
     s = st[bad[0]]

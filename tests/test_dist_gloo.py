@@ -1,0 +1,75 @@
+"""World-size-2 gloo tests (CPU) of the month-sharded path: record all-gather with uneven
+shards, the predictive sum-combine and max-over-ranks timing.  Per-rank records are
+produced by the CPU oracle standing in for the per-rank device kernels; the sharded
+result must equal the single-process one bit for bit (sharding does not change the
+per-month arithmetic)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _records(T, P, rs, seed):
+    rng = np.random.default_rng(seed)
+    rec = rng.standard_normal((T, P, rs))
+    st = (rng.random((T, P)) < 0.9).astype(np.int32)
+    return rec, st
+
+
+def _worker(rank, world, port, T, P, rs, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "fm-returnprediction_amd"))
+    from fmcore import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rec, st = _records(T, P, rs, 5)
+    rows = np.r_[np.full(T // 3, 10), np.full(T - T // 3, 30)]       # uneven month sizes
+    bounds = D.shard_bounds(rows, world)
+    s0, s1 = bounds[rank]
+    counts = [e - s for s, e in bounds]
+    g_rec, g_st = D.gather_records(torch.from_numpy(rec[s0:s1]), torch.from_numpy(st[s0:s1]), counts)
+    ok_gather = bool(np.array_equal(g_rec.numpy(), rec) and np.array_equal(g_st.numpy(), st))
+    # predictive rows: compact index i owned by the rank whose month range holds it
+    months = np.nonzero(st[:, 0])[0]
+    pred_full = np.random.default_rng(9).standard_normal((1, len(months), 4))
+    mine = (months >= s0) & (months < s1)
+    pred = np.where(mine[None, :, None], pred_full, 0.0)
+    pst = mine.astype(np.int32)[None, :]
+    tp, ts = D.combine_predictive(torch.from_numpy(pred.copy()), torch.from_numpy(pst.copy()))
+    ok_pred = bool(np.array_equal(tp.numpy(), pred_full) and (ts.numpy() == 1).all())
+    mx = D.max_over_ranks(float(rank + 1), torch.device("cpu"))
+    q.put((rank, ok_gather, ok_pred, mx, counts))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_records_equal_single_process(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 37, 3, 7, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_gather, ok_pred, mx, counts in out:
+        assert ok_gather and ok_pred, rank
+        assert mx == float(world)
+        assert sum(counts) == 37

@@ -1,0 +1,136 @@
+"""CPU-only tests: the C-ABI library loads and exports every symbol include/fm_hip.h
+declares (no compute call), struct layouts match, and the host-side planning logic
+(validity patterns, chunking, month sharding, Table-2 formatting, synthetic generator)
+behaves as the kernels assume."""
+import os
+import re
+
+import numpy as np
+import pandas as pd
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    txt = open(os.path.join(ROOT, "include", "fm_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(fm_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_library_exports_header_symbols():
+    import ctypes
+    from fmcore import _lib as L
+    lib = L.load()
+    funcs = _header_functions()
+    assert len(funcs) >= 18
+    for f in funcs:
+        assert hasattr(lib, f), f
+        assert f in L.EXPORTED, f"ctypes signature missing for {f}"
+    assert L.version().startswith("libfm_hip")
+    a, b = ctypes.c_int32(), ctypes.c_int32()
+    lib.fm_abi_sizes(ctypes.byref(a), ctypes.byref(b))
+    assert a.value == ctypes.sizeof(L.GramArgs)
+    assert b.value == ctypes.sizeof(L.SolveArgs)
+
+
+def test_library_is_gfx950_code_object():
+    import subprocess
+    from fmcore import _lib as L
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", L.LIB_PATH],
+                         capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    assert "gfx950" in out.stdout + out.stderr
+
+
+def test_compute_entry_points_fail_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from fmcore import engine
+    with pytest.raises(RuntimeError):
+        engine.require_device()
+
+
+def test_plan_patterns_nested_lewellen_models():
+    from fmcore.engine import Model, plan_patterns
+    cols = list(range(16))
+    m1 = Model("m1", 0, [1, 2, 3])
+    m2 = Model("m2", 0, [1, 2, 3, 4, 5, 6, 7])
+    m3 = Model("m3", 0, list(range(1, 15)))
+    f1 = Model("f1", 0, [2, 3, 4, 5, 7])
+    lut, pats = plan_patterns([m1, m2, m3, f1])
+    # M3 valid => M2 valid => M1, F1 valid: 5 non-empty consistent patterns
+    assert sorted(pats) == sorted([0b0001, 0b1000, 0b1001, 0b1011, 0b1111])
+    assert lut[0] == 255 and all(lut[p] != 255 for p in pats)
+    assert cols  # silence
+
+
+def test_make_chunks_cover_segments_exactly():
+    from fmcore.engine import make_chunks
+    seg_off = np.array([0, 0, 5000, 5003, 20000, 20001], dtype=np.int64)
+    seg, rows, off = make_chunks(seg_off, target_chunks=8, min_rows=512)
+    rows = rows.reshape(-1, 2)
+    for s in range(len(seg_off) - 1):
+        mine = rows[off[s]:off[s + 1]]
+        assert (seg[off[s]:off[s + 1]] == s).all()
+        assert mine[0, 0] == seg_off[s] and mine[-1, 1] == seg_off[s + 1]
+        assert (mine[1:, 0] == mine[:-1, 1]).all()
+
+
+def test_shard_bounds_balanced_and_contiguous():
+    from fmcore.dist import shard_bounds
+    rows = np.r_[np.full(50, 100), np.full(50, 300)]
+    b = shard_bounds(rows, 4)
+    assert b[0][0] == 0 and b[-1][1] == 100
+    assert all(b[i][1] == b[i + 1][0] for i in range(3))
+    loads = [rows[s:e].sum() for s, e in b]
+    assert max(loads) - min(loads) <= 300
+
+
+def test_synth_deterministic_and_month_major():
+    from fmcore import synth
+    a = synth.synth_arrays(5, 40, 3, nan_rate=0.1, present_rate=0.8)
+    b = synth.synth_arrays(5, 40, 3, nan_rate=0.1, present_rate=0.8)
+    for k in a:
+        assert np.array_equal(a[k], b[k], equal_nan=a[k].dtype.kind == "f")
+    assert (np.diff(a["month"]) >= 0).all()
+    c = synth.synth_arrays(3, 40, 3, nan_rate=0.1, month0=2)
+    full = synth.synth_arrays(5, 40, 3, nan_rate=0.1)
+    assert np.array_equal(c["retx"], full["retx"][2 * 40:], equal_nan=True)   # shards agree
+
+
+def test_table2_formatting_matches_golden_from_oracle_stats():
+    """The host-side Table-2 string layout (no compute) against the reference's strings."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "fm-returnprediction_amd", "src"))
+    import cases
+    from fmtol import frame_from, load_json, load_npz
+    from oracle import fm_oracle as O
+    import calc_Lewellen_2014 as CL
+    g = load_npz("fm.npz")
+    meta = load_json("fm.json")
+    df = frame_from(g, "in_")
+    subs = O.get_subsets(O.winsorize(df, cases.WINSOR_VARS))
+    stats = {}
+    for mname, (label, xs) in zip(cases.MODELS, zip(CL._LW.MODELS_PREDICTORS, cases.MODELS.values())):
+        for s in cases.SUBSETS:
+            cs = O.run_monthly_cs_regressions(subs[s], "retx", xs)
+            sm = O.fama_macbeth_summary(cs, xs)
+            stats[(label, s)] = {"coef": [sm[f"{x}_coef"] for x in xs], "tstat": [sm[f"{x}_tstat"] for x in xs],
+                                 "mean_R2": sm["mean_R2"], "mean_N": sm["mean_N"]}
+    t2 = CL._format_table_2(stats, cases.SUBSETS)
+    assert [list(i) for i in t2.index] == meta["table2"]["index"]
+    assert [list(c) for c in t2.columns] == meta["table2"]["columns"]
+    assert [[str(x) for x in r] for r in t2.values.tolist()] == meta["table2"]["values"]
+
+
+def test_reference_test_file_collects_nothing():
+    """The reference's own test module defines no test_* function."""
+    import ast
+    src = "/root/reference/src/test_calc_Lewellen_2014.py"
+    if not os.path.exists(src):
+        pytest.skip("reference not mounted")
+    tree = ast.parse(open(src).read())
+    assert not [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name.startswith("test")]
