@@ -129,19 +129,33 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             if (lane == 0) wcnt[w][b] = __popcll(mb);
         }
         __syncthreads();
-        if (tid == 0) {
-            int off = 0;
-            for (int b = 0; b < NB; ++b) {
-                int tot = 0;
-                for (int ww = 0; ww < GNW; ++ww) {
-                    woff[ww][b] = off + tot;
-                    tot += wcnt[ww][b];
-                }
-                btot[b] = tot;
-                boff[b] = off;
-                off += (tot + 3) & ~3;
+        if (w == 0) {
+            // bucket offsets, each bucket padded to a multiple of 4 rows (lane b = bucket b)
+            int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+            if (lane < NB) {
+                c0 = wcnt[0][lane];
+                c1 = wcnt[1][lane];
+                c2 = wcnt[2][lane];
+                c3 = wcnt[3][lane];
             }
-            boff[NB] = off;
+            const int tot = c0 + c1 + c2 + c3;
+            const int pad = (tot + 3) & ~3;
+            int x = pad;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                const int y = __shfl_up(x, o, WAVE);
+                if (lane >= o) x += y;
+            }
+            const int off = x - pad;
+            if (lane < NB) {
+                boff[lane] = off;
+                btot[lane] = tot;
+                woff[0][lane] = off;
+                woff[1][lane] = off + c0;
+                woff[2][lane] = off + c0 + c1;
+                woff[3][lane] = off + c0 + c1 + c2;
+            }
+            if (lane == NB - 1) boff[NB] = off + pad;
         }
         __syncthreads();
         if (bucket >= 0) {

@@ -9,7 +9,7 @@
 //   * the k-th smallest value is bounded above by tau = the k-th smallest of the 256
 //     per-thread minima (k threads each own >= 1 value <= tau), so c_le(tau) >= k+1;
 //   * at most k threads hold values < tau, so the candidates {x < tau} are few (about
-//     k..4k); they are compacted to LDS and bitonic-sorted there.
+//     k); they are compacted to LDS and ranked there by counting (no sort, few barriers).
 // Middle ranks (pandas 0.2/0.5) and any overflow use an exact 8-bit LSD-free radix select
 // (MSB-first histogram narrowing) over the register keys.  Results are the exact order
 // statistics, so the interpolated cut is bit-identical to numpy/pandas given the same
@@ -31,6 +31,7 @@ struct SelSmem {
     uint64_t u64s[SNW];
     double dbl[SNW];
     int ints[8];
+    uint64_t bc[4];
 };
 
 struct SelArgs {
@@ -48,30 +49,6 @@ struct SelArgs {
     double* mean;
     double* sd;
 };
-
-__device__ __forceinline__ void lds_bitonic(uint64_t* a, int M) {
-    for (int k = 2; k <= M; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int t = threadIdx.x; t < (M >> 1); t += ST) {
-                const int i = 2 * t - (t & (j - 1));
-                const int l = i + j;
-                const bool up = (i & k) == 0;
-                const uint64_t x = a[i], y = a[l];
-                if ((x > y) == up) {
-                    a[i] = y;
-                    a[l] = x;
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-__device__ __forceinline__ int pow2ceil(int x) {
-    int p = 1;
-    while (p < x) p <<= 1;
-    return p;
-}
 
 // Exact key of the element at ascending rank `rank` (0-based) among non-SENT keys.
 template <int VPT>
@@ -127,7 +104,19 @@ __device__ __forceinline__ uint64_t radix_rank(const uint64_t (&keys)[VPT], int 
     return prefix;
 }
 
+// Counting rank among LDS values buf[0..M): ascending, ties broken by index (unique ranks).
+__device__ __forceinline__ int lds_rank(const uint64_t* buf, int M, uint64_t v, int self) {
+    int r = 0;
+    for (int u = 0; u < M; ++u) {
+        const uint64_t x = buf[u];
+        r += (x < v || (x == v && u < self)) ? 1 : 0;
+    }
+    return r;
+}
+
 // Keys at ascending ranks ri <= rj (< n) with the tail fast path; block-uniform.
+// tau = the rj-th smallest of the 256 per-thread minima (found by counting ranks, no sort)
+// bounds s[rj] from above; the few keys < tau are compacted to LDS and ranked by counting.
 template <int VPT>
 __device__ __forceinline__ void select_low(const uint64_t (&keys)[VPT], int ri, int rj, uint64_t& ki,
                            uint64_t& kj, SelSmem& sm) {
@@ -138,10 +127,11 @@ __device__ __forceinline__ void select_low(const uint64_t (&keys)[VPT], int ri, 
         for (int v = 0; v < VPT; ++v) m = keys[v] < m ? keys[v] : m;
         __syncthreads();
         sm.buf[threadIdx.x] = m;
+        if (threadIdx.x == 0) sm.bc[0] = SENT;
         __syncthreads();
-        lds_bitonic(sm.buf, ST);
-        const uint64_t tau = sm.buf[rj];
+        if (lds_rank(sm.buf, ST, m, threadIdx.x) == rj) sm.bc[0] = m;
         __syncthreads();
+        const uint64_t tau = sm.bc[0];
         if (tau != SENT) {
             int lt = 0;
 #pragma unroll
@@ -157,12 +147,16 @@ __device__ __forceinline__ void select_low(const uint64_t (&keys)[VPT], int ri, 
 #pragma unroll
                 for (int v = 0; v < VPT; ++v)
                     if (keys[v] < tau) sm.buf[o++] = keys[v];
-                const int M = pow2ceil(c_lt);
-                for (int i = c_lt + threadIdx.x; i < M; i += ST) sm.buf[i] = SENT;
                 __syncthreads();
-                lds_bitonic(sm.buf, M);
-                ki = sm.buf[ri];
-                kj = rj < c_lt ? sm.buf[rj] : tau;
+                for (int i = threadIdx.x; i < c_lt; i += ST) {
+                    const uint64_t v = sm.buf[i];
+                    const int r = lds_rank(sm.buf, c_lt, v, i);
+                    if (r == ri) sm.bc[1] = v;
+                    if (r == rj) sm.bc[2] = v;
+                }
+                __syncthreads();
+                ki = sm.bc[1];
+                kj = rj < c_lt ? sm.bc[2] : tau;
                 __syncthreads();
                 done = true;
             }

@@ -23,7 +23,7 @@ namespace {
 
 constexpr int VT = 256;
 constexpr int VNW = VT / WAVE;
-constexpr int MAXB_LDS = 8192;   // doubles of bucket sums held in LDS (64 KB)
+constexpr int MAXB_LDS = 8192;   // doubles of bucket sums held in LDS (64 KB max)
 constexpr double CHOL_REL = 1e-9;
 constexpr double EIG_REL = 1e-12;
 
@@ -33,67 +33,70 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
+template <int MD>
 struct WaveScratch {
-    double A[32 * 32];   // G, then L (Cholesky) or the Jacobi matrix
-    double V[32 * 32];   // centered S, then Jacobi eigenvectors
-    double sxy[32], sdiag[32], mu[32], b[32], misc[8];
+    double A[MD * MD];   // G, then L (Cholesky) or the Jacobi matrix
+    double V[MD * MD];   // centered S, then Jacobi eigenvectors
+    double sxy[MD], sdiag[MD], mu[MD], b[MD];
 };
 
 // Cyclic Jacobi + pseudo-inverse solve by lane 0 (rare fallback path).
+template <int MD>
 __device__ void jacobi_pinv(double* A, double* V, int K, const double* sxy, double* b) {
     for (int i = 0; i < K; ++i)
-        for (int j = 0; j < K; ++j) V[i * 32 + j] = i == j ? 1.0 : 0.0;
+        for (int j = 0; j < K; ++j) V[i * MD + j] = i == j ? 1.0 : 0.0;
     double frob = 0.0;
     for (int i = 0; i < K; ++i)
-        for (int j = 0; j < K; ++j) frob += A[i * 32 + j] * A[i * 32 + j];
+        for (int j = 0; j < K; ++j) frob += A[i * MD + j] * A[i * MD + j];
     for (int sweep = 0; sweep < 80; ++sweep) {
         double off = 0.0;
         for (int p = 0; p < K; ++p)
-            for (int q = p + 1; q < K; ++q) off += A[p * 32 + q] * A[p * 32 + q];
+            for (int q = p + 1; q < K; ++q) off += A[p * MD + q] * A[p * MD + q];
         if (off <= 1e-34 * frob) break;
         for (int p = 0; p < K; ++p) {
             for (int q = p + 1; q < K; ++q) {
-                const double apq = A[p * 32 + q];
+                const double apq = A[p * MD + q];
                 if (apq == 0.0) continue;
-                const double theta = (A[q * 32 + q] - A[p * 32 + p]) / (2.0 * apq);
+                const double theta = (A[q * MD + q] - A[p * MD + p]) / (2.0 * apq);
                 const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                 const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
                 for (int k = 0; k < K; ++k) {
-                    const double akp = A[k * 32 + p], akq = A[k * 32 + q];
-                    A[k * 32 + p] = c * akp - s * akq;
-                    A[k * 32 + q] = s * akp + c * akq;
+                    const double akp = A[k * MD + p], akq = A[k * MD + q];
+                    A[k * MD + p] = c * akp - s * akq;
+                    A[k * MD + q] = s * akp + c * akq;
                 }
                 for (int k = 0; k < K; ++k) {
-                    const double apk = A[p * 32 + k], aqk = A[q * 32 + k];
-                    A[p * 32 + k] = c * apk - s * aqk;
-                    A[q * 32 + k] = s * apk + c * aqk;
+                    const double apk = A[p * MD + k], aqk = A[q * MD + k];
+                    A[p * MD + k] = c * apk - s * aqk;
+                    A[q * MD + k] = s * apk + c * aqk;
                 }
-                A[p * 32 + q] = 0.0;
-                A[q * 32 + p] = 0.0;
+                A[p * MD + q] = 0.0;
+                A[q * MD + p] = 0.0;
                 for (int k = 0; k < K; ++k) {
-                    const double vkp = V[k * 32 + p], vkq = V[k * 32 + q];
-                    V[k * 32 + p] = c * vkp - s * vkq;
-                    V[k * 32 + q] = s * vkp + c * vkq;
+                    const double vkp = V[k * MD + p], vkq = V[k * MD + q];
+                    V[k * MD + p] = c * vkp - s * vkq;
+                    V[k * MD + q] = s * vkp + c * vkq;
                 }
             }
         }
     }
     double lmax = 0.0;
-    for (int i = 0; i < K; ++i) lmax = fmax(lmax, fabs(A[i * 32 + i]));
+    for (int i = 0; i < K; ++i) lmax = fmax(lmax, fabs(A[i * MD + i]));
     for (int j = 0; j < K; ++j) b[j] = 0.0;
     for (int i = 0; i < K; ++i) {
-        const double l = A[i * 32 + i];
+        const double l = A[i * MD + i];
         if (!(l > EIG_REL * lmax)) continue;
         double proj = 0.0;
-        for (int k = 0; k < K; ++k) proj += V[k * 32 + i] * sxy[k];
+        for (int k = 0; k < K; ++k) proj += V[k * MD + i] * sxy[k];
         proj /= l;
-        for (int j = 0; j < K; ++j) b[j] += proj * V[j * 32 + i];
+        for (int j = 0; j < K; ++j) b[j] += proj * V[j * MD + i];
     }
 }
 
+template <int MD>
 __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
-    __shared__ double bs[MAXB_LDS];
-    __shared__ WaveScratch ws_all[VNW];
+    extern __shared__ double bs[];                 // [nb][zw*zw] bucket sums of this month
+    __shared__ WaveScratch<MD> ws_all[VNW];
     const int s = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
     const int zw = a.zw, zz = zw * zw;
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
         bs[e] = acc;
     }
     __syncthreads();
-    WaveScratch& ws = ws_all[w];
+    WaveScratch<MD>& ws = ws_all[w];
     const int rs = a.pmax + 2;
     for (int p = w; p < a.nprob; p += VNW) {
         const int m = a.prob_model[p], u = a.prob_level[p], nz = a.prob_nz[p];
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
                 const int pid = b / a.nlevels, lvl = b - pid * a.nlevels;
                 if (((a.pattern_models[pid] >> m) & 1u) && lvl >= u) acc += bs[b * zz + off];
             }
-            ws.A[i * 32 + j] = acc;
+            ws.A[i * MD + j] = acc;
         }
         wave_sync();
         const double n = ws.A[0];
@@ -137,103 +140,96 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
         const int K1 = K + 1;
         for (int e = lane; e < K1 * K1; e += WAVE) {
             const int i = e / K1, j = e - (e / K1) * K1;
-            ws.V[i * 32 + j] = ws.A[(1 + i) * 32 + 1 + j] - ws.A[1 + i] * ws.A[1 + j] / n;
+            ws.V[i * MD + j] = ws.A[(1 + i) * MD + 1 + j] - ws.A[1 + i] * ws.A[1 + j] / n;
         }
         if (lane < K1) ws.mu[lane] = ws.A[1 + lane] / n;
-        if (lane < K) {
-            const double sd = ws.A[(1 + lane) * 32 + 1 + lane];
-            ws.sdiag[lane] = sd;   // raw (shifted) second moment, for the constant test
-        }
+        if (lane < K) ws.sdiag[lane] = ws.A[(1 + lane) * MD + 1 + lane];
         wave_sync();
-        if (lane < K) ws.sxy[lane] = ws.V[lane * 32 + K];
+        if (lane < K) ws.sxy[lane] = ws.V[lane * MD + K];
         if (a.moments) {
             double* mo = a.moments + ((int64_t)s * a.nprob + p) * a.mom_stride;
             if (lane == 0) mo[0] = n;
             if (lane < K1) mo[1 + lane] = ws.mu[lane];
             for (int e = lane; e < K1 * K1; e += WAVE)
-                mo[1 + K1 + e] = ws.V[(e / K1) * 32 + (e - (e / K1) * K1)];
+                mo[1 + K1 + e] = ws.V[(e / K1) * MD + (e - (e / K1) * K1)];
         }
-        const double syy = ws.V[K * 32 + K];
+        const double syy = ws.V[K * MD + K];
         if ((a.prob_flags[p] & 1) != 0) {
             bool sus = false;
-            if (lane < K) {
-                const double v = ws.V[lane * 32 + lane];
-                sus = !(v > 1e-10 * ws.sdiag[lane]);
-            }
+            if (lane < K) sus = !(ws.V[lane * MD + lane] > 1e-10 * ws.sdiag[lane]);
             if (__ballot(sus) != 0) st |= FM_ST_CONST_SUSPECT;
         }
-        // ---- Cholesky of Sxx (in A)
+        // ---- Cholesky of Sxx (in A), lanes over the trailing-update entries
         for (int e = lane; e < K * K; e += WAVE) {
             const int i = e / K, j = e - (e / K) * K;
-            ws.A[i * 32 + j] = ws.V[i * 32 + j];
+            ws.A[i * MD + j] = ws.V[i * MD + j];
         }
         wave_sync();
         bool ok = true;
         for (int k = 0; k < K; ++k) {
-            const double piv = ws.A[k * 32 + k];
-            const double orig = ws.V[k * 32 + k];
+            const double piv = ws.A[k * MD + k];
+            const double orig = ws.V[k * MD + k];
             if (!(orig > 0.0) || !(piv > CHOL_REL * orig)) {
                 ok = false;
                 break;
             }
             const double lkk = sqrt(piv);
             wave_sync();
-            if (lane > k && lane < K) ws.A[lane * 32 + k] /= lkk;
-            if (lane == k) ws.A[k * 32 + k] = lkk;
+            if (lane > k && lane < K) ws.A[lane * MD + k] /= lkk;
+            if (lane == k) ws.A[k * MD + k] = lkk;
             wave_sync();
             const int mrem = K - k - 1;
             for (int e = lane; e < mrem * mrem; e += WAVE) {
                 const int i = k + 1 + e / mrem, j = k + 1 + (e - (e / mrem) * mrem);
-                if (j <= i) ws.A[i * 32 + j] -= ws.A[i * 32 + k] * ws.A[j * 32 + k];
+                if (j <= i) ws.A[i * MD + j] -= ws.A[i * MD + k] * ws.A[j * MD + k];
             }
             wave_sync();
         }
+        double bi = 0.0;
         if (ok) {
-            if (lane == 0) {
-                double* y = ws.b;
-                for (int i = 0; i < K; ++i) {
-                    double t = ws.sxy[i];
-                    for (int j = 0; j < i; ++j) t -= ws.A[i * 32 + j] * y[j];
-                    y[i] = t / ws.A[i * 32 + i];
-                }
-                for (int i = K - 1; i >= 0; --i) {
-                    double t = y[i];
-                    for (int j = i + 1; j < K; ++j) t -= ws.A[j * 32 + i] * y[j];
-                    y[i] = t / ws.A[i * 32 + i];
-                }
+            // L y = Sxy then L' b = y, lane i owns row i (values broadcast by shuffles)
+            bi = lane < K ? ws.sxy[lane] : 0.0;
+            for (int j = 0; j < K; ++j) {
+                if (lane == j) bi = bi / ws.A[j * MD + j];
+                const double yj = __shfl(bi, j, WAVE);
+                if (lane > j && lane < K) bi -= ws.A[lane * MD + j] * yj;
+            }
+            for (int j = K - 1; j >= 0; --j) {
+                if (lane == j) bi = bi / ws.A[j * MD + j];
+                const double xj = __shfl(bi, j, WAVE);
+                if (lane < j) bi -= ws.A[j * MD + lane] * xj;
             }
         } else {
             st |= FM_ST_RANK_DEF;
             for (int e = lane; e < K * K; e += WAVE) {
                 const int i = e / K, j = e - (e / K) * K;
-                ws.A[i * 32 + j] = ws.V[i * 32 + j];
+                ws.A[i * MD + j] = ws.V[i * MD + j];
             }
             wave_sync();
-            if (lane == 0) jacobi_pinv(ws.A, ws.V, K, ws.sxy, ws.b);
+            if (lane == 0) jacobi_pinv<MD>(ws.A, ws.V, K, ws.sxy, ws.b);
+            wave_sync();
+            bi = lane < K ? ws.b[lane] : 0.0;
         }
-        wave_sync();
-        if (lane == 0) {
-            double bsxy = 0.0;
-            for (int j = 0; j < K; ++j) bsxy += ws.b[j] * ws.sxy[j];
-            const double r2 = 1.0 - (syy - bsxy) / syy;
-            double icpt = ws.mu[K];
-            for (int j = 0; j < K; ++j) icpt -= ws.b[j] * ws.mu[j];
-            if (a.add_back) {
-                icpt += a.add_back[(int64_t)(zi[K + 1] - 1) * a.nseg + s];
-                for (int j = 0; j < K; ++j) icpt -= ws.b[j] * a.add_back[(int64_t)(zi[1 + j] - 1) * a.nseg + s];
-            }
-            ws.misc[0] = r2;
-            ws.misc[1] = icpt;
-        }
-        wave_sync();
+        // R^2 = 1 - SSR/SST (centered), raw-coordinate intercept
+        double t_sxy = lane < K ? bi * ws.sxy[lane] : 0.0;
+        double t_mu = lane < K ? bi * ws.mu[lane] : 0.0;
+        double t_ab = 0.0;
+        if (a.add_back && lane < K) t_ab = bi * a.add_back[(int64_t)(zi[1 + lane] - 1) * a.nseg + s];
+        t_sxy = wave_sum(t_sxy);
+        t_mu = wave_sum(t_mu);
+        t_ab = wave_sum(t_ab);
+        const double r2 = 1.0 - (syy - t_sxy) / syy;
+        double icpt = ws.mu[K] - t_mu;
+        if (a.add_back) icpt += a.add_back[(int64_t)(zi[K + 1] - 1) * a.nseg + s] - t_ab;
         for (int k = lane; k < rs; k += WAVE) {
             double v = NAN;
-            if (k == 0) v = ws.misc[1];
-            else if (k <= K) v = ws.b[k - 1];
-            else if (k == a.pmax) v = ws.misc[0];
+            if (k == 0) v = icpt;
+            else if (k == a.pmax) v = r2;
             else if (k == a.pmax + 1) v = n;
             a.rec[ro + k] = v;
         }
+        wave_sync();
+        if (lane < K) a.rec[ro + 1 + lane] = bi;
         if (lane == 0) a.status[(int64_t)s * a.nprob + p] = st | FM_ST_FITTED;
         wave_sync();
     }
@@ -303,7 +299,19 @@ extern "C" int fm_solve(const fm_solve_args* args, void* stream) {
     FM_REQUIRE(a.pmax >= 2 && a.pmax <= 32, "fm_solve: pmax must be 2..32");
     FM_REQUIRE(a.moments == nullptr || a.mom_stride > 0, "fm_solve: bad mom_stride");
     if (a.nseg == 0 || a.nprob == 0) return FM_OK;
-    hipLaunchKernelGGL(solve_kernel, dim3(a.nseg), dim3(VT), 0, (hipStream_t)stream, a);
+    const size_t dyn = (size_t)a.npatterns * a.nlevels * a.zw * a.zw * sizeof(double);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)solve_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            MAXB_LDS * (int)sizeof(double));
+        (void)hipFuncSetAttribute((const void*)solve_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            MAXB_LDS * (int)sizeof(double));
+        attr_set = true;
+    }
+    if (a.zw == 16)
+        hipLaunchKernelGGL(solve_kernel<16>, dim3(a.nseg), dim3(VT), dyn, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(solve_kernel<32>, dim3(a.nseg), dim3(VT), dyn, (hipStream_t)stream, a);
     FM_CHECK_LAUNCH("fm_solve");
     return FM_OK;
 }

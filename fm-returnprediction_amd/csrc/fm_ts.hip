@@ -108,67 +108,77 @@ __global__ __launch_bounds__(TT) void summary_kernel(SumArgs a) {
     }
 }
 
+// One workgroup per (problem, coefficient, chunk of RCH output rows): the chunk's window
+// span is staged in LDS, each output is a direct sum over its window (no running-sum drift).
+constexpr int RCH = 1024;
+constexpr int RMAXW = 1024;
+
 __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t r_seg,
                                                      int64_t r_prob, const int32_t* idx,
                                                      const int32_t* count, int nseg, int kmax,
                                                      int window, int minp, double* out) {
-    const int p = blockIdx.y;
-    const int i = blockIdx.x * TT + threadIdx.x;
+    __shared__ double xs[RCH + RMAXW];
+    const int p = blockIdx.y / kmax, k = blockIdx.y - (blockIdx.y / kmax) * kmax;
+    const int c0 = blockIdx.x * RCH;
     const int cnt = count[p];
-    if (i >= cnt) return;
+    if (c0 >= cnt) return;
     const int32_t* ix = idx + (int64_t)p * nseg;
-    const int j0 = i - window + 1 < 0 ? 0 : i - window + 1;
-    for (int k = 0; k < kmax; ++k) {
-        double s = 0.0;
+    const int lo = c0 - window + 1 < 0 ? 0 : c0 - window + 1;
+    const int hi = c0 + RCH < cnt ? c0 + RCH : cnt;
+    for (int j = lo + threadIdx.x; j < hi; j += TT)
+        xs[j - lo] = rec[(int64_t)ix[j] * r_seg + (int64_t)p * r_prob + k];
+    __syncthreads();
+    for (int i = c0 + threadIdx.x; i < hi; i += TT) {
+        const int j0 = i - window + 1 < 0 ? 0 : i - window + 1;
+        double sm = 0.0;
         int c = 0;
         for (int j = j0; j <= i; ++j) {
-            const double x = rec[(int64_t)ix[j] * r_seg + (int64_t)p * r_prob + k];
+            const double x = xs[j - lo];
             if (!isnan(x)) {
-                s += x;
+                sm += x;
                 ++c;
             }
         }
-        out[((int64_t)p * nseg + i) * kmax + k] = c >= minp ? s / (double)c : NAN;
+        out[((int64_t)p * nseg + i) * kmax + k] = c >= minp ? sm / (double)c : NAN;
     }
 }
 
-__global__ __launch_bounds__(TT) void predictive_kernel(const double* mom, int mom_stride,
-                                                        int nseg, int nprob, const int32_t* prob_k,
-                                                        const int32_t* idx, const int32_t* count,
-                                                        const double* roll, int pmax, int lag,
-                                                        int seg_lo, int seg_hi, double* pred,
-                                                        uint32_t* pst) {
-    const int p = blockIdx.y;
-    const int i = blockIdx.x * TT + threadIdx.x;
-    if (i >= nseg) return;
+// One wave per (problem, fitted-month row); lane a owns regressor a.
+__global__ __launch_bounds__(WAVE) void predictive_kernel(const double* mom, int mom_stride,
+                                                          int nseg, int nprob,
+                                                          const int32_t* prob_k, const int32_t* idx,
+                                                          const int32_t* count, const double* roll,
+                                                          int pmax, int lag, int seg_lo, int seg_hi,
+                                                          double* pred, uint32_t* pst) {
+    const int p = blockIdx.y, i = blockIdx.x, lane = threadIdx.x;
     double* o = pred + ((int64_t)p * nseg + i) * 4;
-    uint32_t st = 0;
-    double slope = NAN, r2 = NAN, nn = NAN;
     const int cnt = count[p];
     const int s = i < cnt ? idx[(int64_t)p * nseg + i] : -1;
     if (i < cnt && (s < seg_lo || s >= seg_hi)) {
-        // another rank's month (sharded runs): leave a zero record for the sum-combine
-        o[0] = o[1] = o[2] = o[3] = 0.0;
-        pst[(int64_t)p * nseg + i] = 0;
+        // another rank's month (sharded runs): zero record for the sum-combine
+        if (lane < 4) o[lane] = 0.0;
+        if (lane == 0) pst[(int64_t)p * nseg + i] = 0;
         return;
     }
+    uint32_t st = 0;
+    double slope = NAN, r2 = NAN, nn = NAN;
     if (i < cnt && i >= lag) {
         const int K = prob_k[p];
         const double* c = roll + ((int64_t)p * nseg + (i - lag)) * pmax;
-        bool ok = true;
-        for (int k = 0; k <= K; ++k) ok = ok && !isnan(c[k]);
+        const bool bad = lane <= K && isnan(c[lane]);
         const double* mo = mom + ((int64_t)(s - seg_lo) * nprob + p) * mom_stride;
         const int K1 = K + 1;
         const double n = mo[0];
-        if (ok && n >= 2.0) {
+        if (__ballot(bad) == 0 && n >= 2.0) {
             const double* S = mo + 1 + K1;
-            double bsb = 0.0, bsy = 0.0;
-            for (int a = 0; a < K; ++a) {
+            double tb = 0.0, ty = 0.0;
+            if (lane < K) {
                 double t = 0.0;
-                for (int b = 0; b < K; ++b) t += S[a * K1 + b] * c[1 + b];
-                bsb += c[1 + a] * t;
-                bsy += c[1 + a] * S[a * K1 + K];
+                for (int b = 0; b < K; ++b) t += S[lane * K1 + b] * c[1 + b];
+                tb = c[1 + lane] * t;
+                ty = c[1 + lane] * S[lane * K1 + K];
             }
+            const double bsb = wave_sum(tb), bsy = wave_sum(ty);
             const double syy = S[K * K1 + K];
             slope = bsy / bsb;
             r2 = (bsy * bsy) / (bsb * syy);
@@ -177,11 +187,13 @@ __global__ __launch_bounds__(TT) void predictive_kernel(const double* mom, int m
             if (!(bsb > 0.0)) st |= FM_ST_CONST_COL;
         }
     }
-    o[0] = slope;
-    o[1] = r2;
-    o[2] = nn;
-    o[3] = 0.0;
-    pst[(int64_t)p * nseg + i] = st;
+    if (lane == 0) {
+        o[0] = slope;
+        o[1] = r2;
+        o[2] = nn;
+        o[3] = 0.0;
+        pst[(int64_t)p * nseg + i] = st;
+    }
 }
 
 // Per-row forecast F = c0 + sum_k c_k x_k with the segment's coefficient row (A7).
@@ -248,9 +260,10 @@ extern "C" int fm_rolling_mean(const double* rec, int64_t r_seg, int64_t r_prob,
                                double* out, void* stream) {
     using namespace fm;
     FM_REQUIRE(rec && idx && count && out, "fm_rolling_mean: null pointer");
-    FM_REQUIRE(window >= 1 && min_periods >= 0, "fm_rolling_mean: bad window");
-    if (nprob == 0 || nseg == 0) return FM_OK;
-    dim3 grid((nseg + TT - 1) / TT, nprob);
+    FM_REQUIRE(window >= 1 && window <= RMAXW && min_periods >= 0,
+               "fm_rolling_mean: window must be 1..%d", RMAXW);
+    if (nprob == 0 || nseg == 0 || kmax == 0) return FM_OK;
+    dim3 grid((nseg + RCH - 1) / RCH, nprob * kmax);
     hipLaunchKernelGGL(rolling_kernel, grid, dim3(TT), 0, (hipStream_t)stream, rec, r_seg, r_prob,
                        idx, count, nseg, kmax, window, min_periods, out);
     FM_CHECK_LAUNCH("fm_rolling_mean");
@@ -267,8 +280,8 @@ extern "C" int fm_predictive(const double* moments, int32_t mom_stride, int32_t 
                "fm_predictive: null pointer");
     FM_REQUIRE(lag >= 1, "fm_predictive: lag must be >= 1");
     if (nprob == 0 || nseg == 0) return FM_OK;
-    dim3 grid((nseg + TT - 1) / TT, nprob);
-    hipLaunchKernelGGL(predictive_kernel, grid, dim3(TT), 0, (hipStream_t)stream, moments,
+    dim3 grid(nseg, nprob);
+    hipLaunchKernelGGL(predictive_kernel, grid, dim3(WAVE), 0, (hipStream_t)stream, moments,
                        mom_stride, nseg, nprob, prob_k, idx, count, rolling, pmax, lag, seg_lo,
                        seg_hi, pred, pred_status);
     FM_CHECK_LAUNCH("fm_predictive");

@@ -34,11 +34,14 @@ def test_library_exports_header_symbols():
     assert b.value == ctypes.sizeof(L.SolveArgs)
 
 
-def test_library_is_gfx950_code_object():
+def test_library_is_gfx950_code_object(tmp_path):
+    import shutil
     import subprocess
     from fmcore import _lib as L
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", L.LIB_PATH],
-                         capture_output=True, text=True)
+    lib = tmp_path / "libfm_hip.so"
+    shutil.copy(L.LIB_PATH, lib)   # --offloading extracts the code objects next to its input
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     if out.returncode != 0:
         pytest.skip("llvm-objdump --offloading unavailable")
     assert "gfx950" in out.stdout + out.stderr
