@@ -84,24 +84,28 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     for (int64_t t0 = r0; t0 < r1; t0 += GT) {
         const int64_t row = t0 + tid;
         const bool inr = row < r1;
+        // Unconditional loads (row and column clamped in range, results masked after):
+        // a load under a runtime condition makes hipcc wait vmcnt(0) per load.
+        const int64_t lrow = inr ? row : r1 - 1;
+        double xv[ZW - 1];
+#pragma unroll
+        for (int c = 0; c < ZW - 1; ++c) {
+            const int cc = c < ncols ? c : ncols - 1;
+            xv[c] = a.cols[(int64_t)cc * a.col_stride + lrow];
+        }
         double z[ZW];
         z[0] = 1.0;
         uint32_t nn = 0, infb = 0;
 #pragma unroll
         for (int c = 0; c < ZW - 1; ++c) {
-            double v = 0.0;
-            if (c < ncols && inr) {
-                double x = a.cols[(int64_t)c * a.col_stride + row];
-                const double l = prm[0][c], h = prm[1][c];
-                if (x < l) x = l;   // pandas clip semantics: NaN stays, NaN bound ignored
-                if (x > h) x = h;
-                if (!isnan(x)) {
-                    nn |= 1u << c;
-                    if (isinf(x)) infb |= 1u << c;
-                    v = (x - prm[2][c]) * prm[3][c];
-                }
-            }
-            z[1 + c] = v;
+            double x = xv[c];
+            const double l = prm[0][c], h = prm[1][c];
+            if (x < l) x = l;   // pandas clip semantics: NaN stays, NaN bound ignored
+            if (x > h) x = h;
+            const bool ok = c < ncols && inr && !isnan(x);
+            nn |= ok ? 1u << c : 0u;
+            infb |= (ok && isinf(x)) ? 1u << c : 0u;
+            z[1 + c] = ok ? (x - prm[2][c]) * prm[3][c] : 0.0;
         }
         uint32_t pat = 0;
         for (int m = 0; m < nmodels; ++m)
@@ -265,8 +269,8 @@ extern "C" int fm_gram(const fm_gram_args* args, void* stream) {
             return FM_ETOOBIG;
         }
     } else {
-        if (nb <= 1) launch_gram<2, 1, 2>(a, st);
-        else if (nb <= 4) launch_gram<2, 4, 2>(a, st);
+        if (nb <= 1) launch_gram<2, 1, 1>(a, st);
+        else if (nb <= 4) launch_gram<2, 4, 1>(a, st);
         else if (nb <= 8) launch_gram<2, 8, 1>(a, st);
         else {
             set_error("fm_gram: %d buckets exceed 8 for >15 columns", nb);

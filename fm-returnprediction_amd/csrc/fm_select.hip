@@ -239,17 +239,30 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
     const double* src = a.cols + (int64_t)c * a.col_stride + r0;
     uint64_t keys[VPT];
     int cnt = 0;
+    // Unconditional loads (index clamped, masked after): a load under a runtime condition
+    // makes hipcc wait vmcnt(0) per load and serializes the HBM round trips.
+    const int last = L > 0 ? L - 1 : 0;
+    double xv[VPT];
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
         const int idx = threadIdx.x + v * ST;
-        uint64_t k = SENT;
-        if (idx < L) {
-            const double x = src[idx];
-            const bool on = a.mask == nullptr || a.mask[r0 + idx] != 0;
-            if (on && !isnan(x)) k = dkey(x);
+        xv[v] = L > 0 ? src[idx < L ? idx : last] : NAN;
+    }
+    uint8_t mk[VPT];
+    if (a.mask != nullptr) {
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            const int idx = threadIdx.x + v * ST;
+            mk[v] = L > 0 ? a.mask[r0 + (idx < L ? idx : last)] : 0;
         }
+    }
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const int idx = threadIdx.x + v * ST;
+        const bool on = idx < L && (a.mask == nullptr || mk[v] != 0) && !isnan(xv[v]);
+        const uint64_t k = on ? dkey(xv[v]) : SENT;
         keys[v] = k;
-        cnt += k != SENT ? 1 : 0;
+        cnt += on ? 1 : 0;
     }
     const int n = block_sum<SNW>(cnt, sm.ints);
     double lo = NAN, hi = NAN;
