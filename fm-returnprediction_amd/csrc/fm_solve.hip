@@ -283,6 +283,112 @@ __global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t s
     if (threadIdx.x == 0 && any_const) status[(int64_t)s * nprob + p] |= FM_ST_CONST_COL;
 }
 
+// inf in y (statsmodels keeps the month): params = pinv(X) @ y, so each coefficient is the
+// IEEE sum of pinv[j,i] * y_i; with y_i = +-inf the finite rows do not matter and the
+// result is +inf, -inf or NaN (mixed signs, or 0*inf).  pinv[:,i] for the slopes is
+// Sxx^{-1}(x_i - xbar) and for the intercept 1/n - xbar'Sxx^{-1}(x_i - xbar).  One
+// workgroup per flagged (month, problem); R^2 becomes NaN as in statsmodels.
+__global__ __launch_bounds__(VT) void infy_kernel(const double* cols, int64_t stride,
+                                                  const int64_t* seg_off, int nseg, const double* lo,
+                                                  const double* hi, const double* shift,
+                                                  const double* inv_scale, const double* add_back,
+                                                  const uint8_t* level, int nprob,
+                                                  const int32_t* prob_level, const int32_t* prob_z,
+                                                  const int32_t* prob_nz, const int32_t* pairs,
+                                                  const double* moments, int mom_stride, int pmax,
+                                                  double* rec, uint32_t* status) {
+    __shared__ double Lm[32 * 32];
+    __shared__ double mu[32], xb[32];
+    __shared__ unsigned bits[32];
+    __shared__ int okf;
+    const int s = pairs[2 * blockIdx.x], p = pairs[2 * blockIdx.x + 1];
+    const int nz = prob_nz[p], K = nz - 2, K1 = K + 1, u = prob_level[p];
+    const int* zi = prob_z + p * 32;
+    const double* mo = moments + ((int64_t)s * nprob + p) * mom_stride;
+    const double n = mo[0];
+    for (int e = threadIdx.x; e < K * K; e += VT) Lm[(e / K) * 32 + e % K] = mo[1 + K1 + (e / K) * K1 + e % K];
+    if (threadIdx.x < K1) mu[threadIdx.x] = mo[1 + threadIdx.x];
+    if (threadIdx.x < 32) bits[threadIdx.x] = 0u;
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int c = zi[1 + threadIdx.x] - 1;
+        xb[threadIdx.x] = mu[threadIdx.x] + (add_back ? add_back[(int64_t)c * nseg + s] : 0.0);
+    }
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        for (int k = 0; k < K && ok; ++k) {
+            double d = Lm[k * 32 + k];
+            for (int j = 0; j < k; ++j) d -= Lm[k * 32 + j] * Lm[k * 32 + j];
+            if (!(d > 0.0)) { ok = 0; break; }
+            d = sqrt(d);
+            Lm[k * 32 + k] = d;
+            for (int i = k + 1; i < K; ++i) {
+                double t = Lm[i * 32 + k];
+                for (int j = 0; j < k; ++j) t -= Lm[i * 32 + j] * Lm[k * 32 + j];
+                Lm[i * 32 + k] = t / d;
+            }
+        }
+        okf = ok;
+    }
+    __syncthreads();
+    if (!okf) return;   // rank-deficient with an inf y: left as computed (NaN)
+    const int64_t r0 = seg_off[s], r1 = seg_off[s + 1];
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += VT) {
+        if (level && (int)level[r] < u) continue;
+        double v[32];
+        bool valid = true;
+        for (int q = 1; q < nz; ++q) {
+            const int c = zi[q] - 1;
+            double x = cols[(int64_t)c * stride + r];
+            if (lo) {
+                const double l = lo[(int64_t)c * nseg + s], h = hi[(int64_t)c * nseg + s];
+                if (x < l) x = l;
+                if (x > h) x = h;
+            }
+            if (isnan(x)) valid = false;
+            v[q - 1] = x;
+        }
+        if (!valid || !isinf(v[K])) continue;
+        const double y = v[K];
+        double d[32];
+        for (int j = 0; j < K; ++j) {
+            const int c = zi[1 + j] - 1;
+            double x = v[j];
+            if (shift) x -= shift[(int64_t)c * nseg + s];
+            if (inv_scale) x *= inv_scale[(int64_t)c * nseg + s];
+            d[j] = x - mu[j];
+        }
+        for (int i = 0; i < K; ++i) {          // L w = d
+            double t = d[i];
+            for (int j = 0; j < i; ++j) t -= Lm[i * 32 + j] * d[j];
+            d[i] = t / Lm[i * 32 + i];
+        }
+        for (int i = K - 1; i >= 0; --i) {     // L' c = w
+            double t = d[i];
+            for (int j = i + 1; j < K; ++j) t -= Lm[j * 32 + i] * d[j];
+            d[i] = t / Lm[i * 32 + i];
+        }
+        double c0 = 1.0 / n;
+        for (int j = 0; j < K; ++j) c0 -= xb[j] * d[j];
+        for (int j = 0; j <= K; ++j) {
+            const double term = (j == 0 ? c0 : d[j - 1]) * y;
+            const unsigned b = isnan(term) ? 4u : (term > 0.0 ? 1u : 2u);
+            atomicOr(&bits[j], b);
+        }
+    }
+    __syncthreads();
+    const int64_t ro = ((int64_t)s * nprob + p) * (pmax + 2);
+    if (threadIdx.x <= K) {
+        const unsigned b = bits[threadIdx.x];
+        if (b != 0u) {
+            double val = NAN;
+            if (!(b & 4u) && b != 3u) val = (b & 1u) ? INFINITY : -INFINITY;
+            rec[ro + threadIdx.x] = val;
+        }
+    }
+    if (threadIdx.x == 0) rec[ro + pmax] = NAN;
+}
+
 }  // namespace
 }  // namespace fm
 
@@ -331,5 +437,24 @@ extern "C" int fm_const_check(const double* cols, int64_t col_stride, int32_t nc
                        col_stride, ncols, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
                        prob_nz, pairs, status);
     FM_CHECK_LAUNCH("fm_const_check");
+    return FM_OK;
+}
+
+extern "C" int fm_inf_y_fix(const double* cols, int64_t col_stride, const int64_t* seg_off,
+                            int32_t nseg, const double* lo, const double* hi, const double* shift,
+                            const double* inv_scale, const double* add_back, const uint8_t* level,
+                            int32_t nprob, const int32_t* prob_level, const int32_t* prob_z,
+                            const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
+                            const double* moments, int32_t mom_stride, int32_t pmax, double* rec,
+                            uint32_t* status, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(cols && seg_off && prob_level && prob_z && prob_nz && pairs && moments && rec && status,
+               "fm_inf_y_fix: null pointer");
+    FM_REQUIRE((lo == nullptr) == (hi == nullptr), "fm_inf_y_fix: lo/hi must both be set or NULL");
+    if (npairs == 0) return FM_OK;
+    hipLaunchKernelGGL(infy_kernel, dim3(npairs), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
+                       seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
+                       prob_z, prob_nz, pairs, moments, mom_stride, pmax, rec, status);
+    FM_CHECK_LAUNCH("fm_inf_y_fix");
     return FM_OK;
 }

@@ -70,6 +70,8 @@ _SIGS = {
     "fm_solve": (_i32, [C.POINTER(SolveArgs), _p]),
     "fm_const_check": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _i32, _p, _p, _p, _p,
                               _i32, _p, _p]),
+    "fm_inf_y_fix": (_i32, [_p, _i64, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32,
+                            _p, _i32, _i32, _p, _p, _p]),
     "fm_ts_compact": (_i32, [_p, _i64, _i64, _i32, _i32, _p, _p, _p]),
     "fm_ts_summary": (_i32, [_p, _i64, _i64, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
                              _p, _p]),

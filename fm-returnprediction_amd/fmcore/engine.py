@@ -426,7 +426,8 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
         patm = t(np.array(pats, dtype=np.int64).astype(np.uint32).view(np.int32))
         grec = torch.empty((T, len(gp), rs), dtype=torch.float64, device=dev)
         gst = torch.zeros((T, len(gp)), dtype=torch.int32, device=dev)
-        gmom = torch.empty((T, len(gp), mom_stride), dtype=torch.float64, device=dev) if moments else None
+        # centered moments are always produced: the inf-in-y fix reads them
+        gmom = torch.empty((T, len(gp), mom_stride), dtype=torch.float64, device=dev)
         sa = L.SolveArgs(
             partial=partial.data_ptr(), seg_chunk_off=plan.seg_chunk_off.data_ptr(), nseg=T, zw=zw,
             nlevels=nlevels, npatterns=len(pats), pattern_models=patm.data_ptr(), nprob=len(gp),
@@ -437,12 +438,23 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
         _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
         idx = torch.tensor([k for k, _ in gp], dtype=torch.int64, device=dev)
         if len(groups) == 1:
-            rec, status, mom = grec, gst, gmom
+            rec, status = grec, gst
+            mom = gmom if moments else None
         else:
             rec.index_copy_(1, idx, grec)
             status.index_copy_(1, idx, gst)
             if moments:
                 mom.index_copy_(1, idx, gmom)
+        # inf in y: statsmodels' pinv(X) @ y gives +-inf / NaN coefficients (rare; one sync)
+        iy = (((gst & L.FM_ST_FITTED) != 0) & ((gst & L.FM_ST_INF_IN_Y) != 0)).nonzero()
+        if iy.numel():
+            pairs = iy.to(torch.int32).contiguous()
+            _kcall("fm_inf_y_fix", "fm_inf_y_fix", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
+                   _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), len(gp),
+                   pl.data_ptr(), pzt.data_ptr(), pnzt.data_ptr(), pairs.data_ptr(), pairs.shape[0],
+                   gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), _stream())
+            if len(groups) > 1:
+                rec.index_copy_(1, idx, grec)
         # exact nonzero-constant test where the Gram flagged a near-zero variance
         if const_check:
             sus = ((gst & L.FM_ST_CONST_SUSPECT) != 0).nonzero()

@@ -19,6 +19,8 @@
  *                      over models x universes in one read of the panel
  *   fm_solve        <- sm.OLS(Y, X).fit() params / rsquared / N and the N<K+1 skip
  *                      (src/regressions.py:52-72; src/calc_Lewellen_2014.py:914-921)
+ *   fm_inf_y_fix    <- pinv(X) @ y with an infinite return: +-inf/NaN params, NaN R2
+ *                      (statsmodels behaviour inside src/regressions.py:57-64)
  *   fm_const_check  <- add_constant(has_constant='skip') nonzero-constant detection
  *                      (src/regressions.py:50, which leads to IndexError at :71)
  *   fm_ts_compact, fm_ts_summary <- fama_macbeth_summary + newey_west_mean_se
@@ -149,6 +151,13 @@ int fm_const_check(const double* cols, int64_t col_stride, int32_t ncols,
                    int32_t nprob, const int32_t* prob_level, const int32_t* prob_z,
                    const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
                    uint32_t* status, void* stream);
+
+int fm_inf_y_fix(const double* cols, int64_t col_stride, const int64_t* seg_off, int32_t nseg,
+                 const double* lo, const double* hi, const double* shift, const double* inv_scale,
+                 const double* add_back, const uint8_t* level, int32_t nprob,
+                 const int32_t* prob_level, const int32_t* prob_z, const int32_t* prob_nz,
+                 const int32_t* pairs, int32_t npairs, const double* moments, int32_t mom_stride,
+                 int32_t pmax, double* rec, uint32_t* status, void* stream);
 
 int fm_ts_compact(const uint32_t* status, int64_t s_seg, int64_t s_prob, int32_t nseg,
                   int32_t nprob, int32_t* idx, int32_t* count, void* stream);

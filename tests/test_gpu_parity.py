@@ -167,8 +167,6 @@ def test_edge_cases_golden(R):
         assert list(got.columns) == m["columns"], name
         exp = frame_from(g, name + "|out_")
         assert np.array_equal(got["N"].values, exp["N"].values), name
-        if name == "inf_y":
-            continue   # tracked in test_inf_in_y_xfail
         for c in got.columns[2:]:
             assert_series_close(got[c].values, exp[c].values, f"{name} {c}")
         summ = R.fama_macbeth_summary(got, xs, "mthcaldt", 4)
@@ -177,9 +175,7 @@ def test_edge_cases_golden(R):
             assert scalar_close(summ[k], v), (name, k, summ[k], v)
 
 
-@pytest.mark.xfail(reason="inf in y: statsmodels returns +-inf slopes via pinv(X)@y; the "
-                          "normal-equation path returns NaN (DESIGN.md, known divergence)")
-def test_inf_in_y_xfail(R):
+def test_inf_in_y_matches_pinv_semantics(R):
     g = load_npz("edge.npz")
     name, df, xs = [c for c in cases.edge_cases() if c[0] == "inf_y"][0]
     got = R.run_monthly_cs_regressions(df, "retx", xs, "mthcaldt")
