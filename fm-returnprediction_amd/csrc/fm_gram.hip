@@ -21,6 +21,7 @@
 // Gram is the sum over patterns that contain m and levels >= the problem's universe,
 // restricted to m's columns.  One HBM read of the panel serves every model x universe.
 #include <math.h>
+#include <stdlib.h>
 
 #include "fm_common.h"
 
@@ -32,7 +33,7 @@ constexpr int GNW = GT / WAVE;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-template <int NT, int NB, int MINW>
+template <int NT, int NB, int MINW, bool PF>
 __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     constexpr int ZW = 16 * NT;
     constexpr int RS = ZW + 1;          // LDS row stride (doubles): conflict-free scatter
@@ -81,20 +82,30 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     }
     uint32_t fl = 0;   // bit 2m: inf in a regressor of model m; bit 2m+1: inf in its y
 
-    for (int64_t t0 = r0; t0 < r1; t0 += GT) {
-        const int64_t row = t0 + tid;
-        const bool inr = row < r1;
-        // Unconditional loads (row and column clamped in range, results masked after):
-        // a load under a runtime condition makes hipcc wait vmcnt(0) per load.
-        const int64_t lrow = inr ? row : r1 - 1;
-        double xv[ZW - 1];
+    // Software pipeline: the next tile's loads are issued before this tile's sort and
+    // MFMA work.  Loads are unconditional (row and column clamped in range, results masked
+    // after): a load under a runtime condition makes hipcc wait vmcnt(0) per load.
+    double xv[ZW - 1];
+    {
+        const int64_t lrow = r0 + tid < r1 ? r0 + tid : r1 - 1;
 #pragma unroll
         for (int c = 0; c < ZW - 1; ++c) {
             const int cc = c < ncols ? c : ncols - 1;
             xv[c] = a.cols[(int64_t)cc * a.col_stride + lrow];
         }
-        double z[ZW];
-        z[0] = 1.0;
+    }
+    for (int64_t t0 = r0; t0 < r1; t0 += GT) {
+        const int64_t row = t0 + tid;
+        const bool inr = row < r1;
+        double xn[ZW - 1];
+        if (PF) {
+            const int64_t nrow = t0 + GT + tid < r1 ? t0 + GT + tid : r1 - 1;
+#pragma unroll
+            for (int c = 0; c < ZW - 1; ++c) {
+                const int cc = c < ncols ? c : ncols - 1;
+                xn[c] = a.cols[(int64_t)cc * a.col_stride + nrow];
+            }
+        }
         uint32_t nn = 0, infb = 0;
 #pragma unroll
         for (int c = 0; c < ZW - 1; ++c) {
@@ -105,7 +116,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             const bool ok = c < ncols && inr && !isnan(x);
             nn |= ok ? 1u << c : 0u;
             infb |= (ok && isinf(x)) ? 1u << c : 0u;
-            z[1 + c] = ok ? (x - prm[2][c]) * prm[3][c] : 0.0;
+            xv[c] = x;
         }
         uint32_t pat = 0;
         for (int m = 0; m < nmodels; ++m)
@@ -163,9 +174,12 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         }
         __syncthreads();
         if (bucket >= 0) {
+            // z = [1, (x - shift) * inv_scale ..., 0 pad], NaN -> 0
             double* dst = tile + (woff[w][bucket] + rank) * RS;
+            dst[0] = 1.0;
 #pragma unroll
-            for (int c = 0; c < ZW; ++c) dst[c] = z[c];
+            for (int c = 0; c < ZW - 1; ++c)
+                dst[1 + c] = ((nn >> c) & 1u) ? (xv[c] - prm[2][c]) * prm[3][c] : 0.0;
         }
         if (tid < NB * 3) {
             const int b = tid / 3, k = tid - 3 * (tid / 3);
@@ -193,6 +207,17 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             }
         }
         __syncthreads();
+        if (PF) {
+#pragma unroll
+            for (int c = 0; c < ZW - 1; ++c) xv[c] = xn[c];
+        } else {
+            const int64_t nrow = t0 + GT + tid < r1 ? t0 + GT + tid : r1 - 1;
+#pragma unroll
+            for (int c = 0; c < ZW - 1; ++c) {
+                const int cc = c < ncols ? c : ncols - 1;
+                xv[c] = a.cols[(int64_t)cc * a.col_stride + nrow];
+            }
+        }
     }
 
     // ---- inf flags (rare): one atomic per wave per model
@@ -237,7 +262,15 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 
 template <int NT, int NB, int MINW>
 void launch_gram(const fm_gram_args& a, hipStream_t st) {
-    hipLaunchKernelGGL((gram_kernel<NT, NB, MINW>), dim3(a.nchunks), dim3(GT), 0, st, a);
+    // FM_GRAM_PREFETCH=0 selects the non-pipelined variant (A/B measurements)
+    static const int pf = [] {
+        const char* e = getenv("FM_GRAM_PREFETCH");
+        return e ? atoi(e) : 1;
+    }();
+    if (pf)
+        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true>), dim3(a.nchunks), dim3(GT), 0, st, a);
+    else
+        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false>), dim3(a.nchunks), dim3(GT), 0, st, a);
 }
 
 }  // namespace
