@@ -79,6 +79,8 @@ _SIGS = {
     "fm_predictive": (_i32, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p,
                              _p]),
     "fm_forecast": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p]),
+    "fm_segment_moments": (_i32, [_p, _i64, _i32, _p, _i32, _p, _i32, _i32, _p, _p, _p, _p]),
+    "fm_distinct_count": (_i32, [_p, _i64, _p, _i64, _i32, _p, _i32, _i32, _i64, _i64, _p, _p, _p]),
     "fm_gen_panel": (_i32, [C.c_uint64, _i64, _i32, _i32, _f64, _f64, _p, _i64, _p, _p, _p]),
     "fm_stream_probe": (_i32, [_p, _i64, _p, _p]),
 }

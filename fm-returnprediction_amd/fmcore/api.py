@@ -82,5 +82,16 @@ def records_summary(values, nw_lags=4):
             s.nobs[0].cpu().numpy())
 
 
+def records_summary_device(vals, nw_lags=0):
+    """Device FM summaries (NaN-skipping means) of the columns of a [T, k] device tensor."""
+    T, k = vals.shape
+    rec = vals.contiguous().view(T, 1, k)
+    status = torch.full((T, 1), L.FM_ST_FITTED, dtype=torch.int32, device=vals.device)
+    ix = E.ts_compact(status, 1, 1, T, 1)
+    s = E.ts_summary(rec, k, k, ix, T, 1, k, nw_lags)
+    return (s.mean[0].cpu().numpy(), s.se[0].cpu().numpy(), s.tstat[0].cpu().numpy(),
+            s.nobs[0].cpu().numpy())
+
+
 def sorted_frame(df):
     return df.sort_values(["mthcaldt", "permno"]).copy()

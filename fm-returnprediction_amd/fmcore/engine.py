@@ -561,6 +561,36 @@ def forecast(panel: DevicePanel, coef, cols=None):
     return out
 
 
+def segment_moments(panel: DevicePanel, level=None, min_level=0, finite_only=True, cols=None):
+    """Per (column, month) count, mean and ddof=1 std of the non-missing values."""
+    src = panel.cols if cols is None else cols
+    C, T = src.shape[0], panel.nseg
+    cnt = torch.empty((C, T), dtype=torch.int32, device=src.device)
+    mean = torch.empty((C, T), dtype=torch.float64, device=src.device)
+    sd = torch.empty_like(mean)
+    _kcall("fm_segment_moments", "fm_segment_moments", src.data_ptr(), src.stride(0), C,
+           panel.seg_off.data_ptr(), T, _ptr(level), int(min_level), int(bool(finite_only)),
+           cnt.data_ptr(), mean.data_ptr(), sd.data_ptr(), _stream())
+    return cnt, mean, sd
+
+
+def distinct_count(ids, cols, level=None, min_level=0, finite_only=True):
+    """Number of distinct ids among rows where each column is present -> int32 [C]."""
+    C, n = cols.shape
+    dev = cols.device
+    out = torch.empty(C, dtype=torch.int32, device=dev)
+    if n == 0:
+        out.zero_()
+        return out
+    lo = int(ids.min().item())
+    rng = int(ids.max().item()) - lo + 1
+    bitmap = torch.empty((C, (rng + 31) // 32), dtype=torch.int32, device=dev)
+    _kcall("fm_distinct_count", "fm_distinct_count", ids.data_ptr(), n, cols.data_ptr(), cols.stride(0), C,
+           _ptr(level), int(min_level), int(bool(finite_only)), lo, rng, bitmap.data_ptr(), out.data_ptr(),
+           _stream())
+    return out
+
+
 def stream_probe(t):
     out = torch.zeros(1, dtype=torch.float64, device=t.device)
     _kcall("fm_stream_probe", "fm_stream_probe", t.data_ptr(), t.numel(), out.data_ptr(), _stream())

@@ -4,13 +4,14 @@ src/calc_Lewellen_2014.py, on MI355X.
 Mirrored (same names, signatures, return types and row/column/index order):
   winsorize        reference :505-529   per-month 1/99 cuts (fm_select_cuts) + clip (fm_clip)
   get_subsets      reference :44-112    NYSE me breakpoints (fm_select_cuts, pandas lerp)
+  build_table_1    reference :577-670   monthly moments + distinct permnos on device (§8(f) row 1)
   build_table_2    reference :674-868   9 FM passes batched into one Gram pass on device
   create_figure_1  reference :871-957   F1 OLS + 120-month rolling means on device
 Extensions the north star names (not in the reference; parity unpinned):
   standardize, monthly_coefficients, rolling_coefficients, expected_return_forecasts,
   predictive_slope_regressions, lewellen_pipeline.
-The firm-characteristic builders (calc_*), Table 1, data pulls and LaTeX output of the
-reference are outside this drop-in (scope).
+The firm-characteristic builders (calc_*), data pulls and LaTeX output of the reference are
+outside this drop-in (scope).
 """
 import os
 import sys
@@ -127,6 +128,50 @@ def standardize(crsp_comp: pd.DataFrame, varlist: list, date_col: str = "mthcald
         col[panel.order] = z[i]
         df[v] = col
     return df
+
+
+# ------------------------------------------------------------------------------------------
+# Table 1
+# ------------------------------------------------------------------------------------------
+def build_table_1(subsets_crsp_comp: dict, variables_dict: dict) -> pd.DataFrame:
+    """Lewellen Table 1: per universe and variable, the time-series averages of the monthly
+    cross-sectional mean and std (ddof=1) after inf->NaN and dropna, and the number of
+    distinct permnos (reference src/calc_Lewellen_2014.py:577-670)."""
+    import torch
+    partial = []
+    for subset_name, df_subset in subsets_crsp_comp.items():
+        present = list(dict.fromkeys(c for c in variables_dict.values() if c in df_subset.columns))
+        stats = {}
+        if present:
+            arrays = [_api.as_f64(df_subset[c]) for c in present]
+            panel = _E.panel_from_arrays(arrays, present, df_subset["mthcaldt"].values)
+            cnt, mean, sd = _E.segment_moments(panel, finite_only=True)
+            T = panel.nseg
+            C = len(present)
+            vals = torch.cat([mean, sd], dim=0).t().contiguous()           # [T, 2C]
+            if T:
+                am, _, _, an = _api.records_summary_device(vals, nw_lags=0)
+            else:
+                am, an = np.full(2 * C, np.nan), np.zeros(2 * C, dtype=np.int64)
+            dev = panel.cols.device
+            allv = torch.from_numpy(np.stack(arrays)).to(dev)                # every row, NaT months too
+            ids = torch.from_numpy(df_subset["permno"].to_numpy(dtype=np.int64)).to(dev)
+            nuniq = _E.distinct_count(ids, allv, finite_only=True).cpu().numpy()
+            tot = cnt.sum(dim=1).cpu().numpy()
+            for i, c in enumerate(present):
+                stats[c] = (tot[i], am[i] if an[i] else np.nan, am[C + i] if an[C + i] else np.nan,
+                            int(nuniq[i]))
+        rows = []
+        for var_label, var_col in variables_dict.items():
+            st = stats.get(var_col)
+            if st is None or (st[0] == 0 and st[3] == 0):
+                rows.append({"Column": var_label, "Avg": np.nan, "Std": np.nan, "N": np.nan})
+            else:
+                rows.append({"Column": var_label, "Avg": st[1], "Std": st[2], "N": st[3]})
+        part = pd.DataFrame(rows).set_index("Column")
+        part.columns = pd.MultiIndex.from_product([[subset_name], part.columns])
+        partial.append(part)
+    return pd.concat(partial, axis=1)
 
 
 # ------------------------------------------------------------------------------------------

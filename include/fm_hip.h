@@ -30,6 +30,8 @@
  *   fm_predictive   <- build-defined extension: lagged-rolling-coefficient forecasts and
  *                      predictive-slope regressions (paper Table 3; no reference line)
  *   fm_forecast     <- build-defined extension A7: per-row F = a_{t-1} + b_{t-1}'x_t
+ *   fm_segment_moments, fm_distinct_count <- build_table_1's monthly mean / std(ddof=1)
+ *                      and permno nunique (src/calc_Lewellen_2014.py:623-646)
  *   fm_gen_panel    <- (bench/test data) counter-based synthetic panel, bit-identical to
  *                      fmcore/synth.py
  *
@@ -179,6 +181,16 @@ int fm_predictive(const double* moments, int32_t mom_stride, int32_t nseg, int32
 int fm_forecast(const double* cols, int64_t col_stride, int32_t K, const int64_t* seg_off,
                 int32_t nseg, int64_t nrows, const double* coef, int32_t coef_stride,
                 double* out, void* stream);
+
+int fm_segment_moments(const double* cols, int64_t col_stride, int32_t ncols,
+                       const int64_t* seg_off, int32_t nseg, const uint8_t* level,
+                       int32_t min_level, int32_t finite_only, int32_t* count, double* mean,
+                       double* sd, void* stream);
+
+int fm_distinct_count(const int64_t* ids, int64_t nrows, const double* cols, int64_t col_stride,
+                      int32_t ncols, const uint8_t* level, int32_t min_level, int32_t finite_only,
+                      int64_t id_lo, int64_t id_range, uint32_t* bitmap, int32_t* out,
+                      void* stream);
 
 int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
                  double nan_rate, double nyse_rate, double* cols, int64_t col_stride,

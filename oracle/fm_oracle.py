@@ -142,6 +142,40 @@ def get_subsets(crsp_comp):
     }
 
 
+def build_table_1(subsets, variables_dict):
+    """src/calc_Lewellen_2014.py:577-670: per subset and variable, inf->NaN, dropna, monthly
+    mean/std(ddof=1), their time-series means, distinct permnos; MultiIndex columns."""
+    parts = []
+    for name, d in subsets.items():
+        rows = []
+        for label, col in variables_dict.items():
+            if col not in d.columns:
+                rows.append({"Column": label, "Avg": np.nan, "Std": np.nan, "N": np.nan})
+                continue
+            v = d[col].to_numpy(dtype=np.float64).copy()
+            v[np.isinf(v)] = np.nan
+            keep = ~np.isnan(v)
+            if not keep.any():
+                rows.append({"Column": label, "Avg": np.nan, "Std": np.nan, "N": np.nan})
+                continue
+            months = d["mthcaldt"].values[keep]
+            vv = v[keep]
+            uniq, order, bounds = month_groups(months)
+            means, stds = [], []
+            for t in range(len(uniq)):
+                x = vv[order[bounds[t]:bounds[t + 1]]]
+                means.append(x.mean())
+                stds.append(x.std(ddof=1) if x.size > 1 else np.nan)
+            means, stds = np.array(means), np.array(stds)
+            rows.append({"Column": label, "Avg": np.nanmean(means) if means.size else np.nan,
+                         "Std": np.nanmean(stds) if np.isfinite(stds).any() else np.nan,
+                         "N": len(np.unique(d["permno"].values[keep]))})
+        p = pd.DataFrame(rows).set_index("Column")
+        p.columns = pd.MultiIndex.from_product([[name], p.columns])
+        parts.append(p)
+    return pd.concat(parts, axis=1)
+
+
 # ----------------------------------------------------------------------------------------
 # Cross-sectional OLS (statsmodels semantics restated)
 # ----------------------------------------------------------------------------------------

@@ -98,7 +98,7 @@ class RecordingSM:
 
 def load_calc(plt_obj, sm_obj):
     src = open(os.path.join(REF, "calc_Lewellen_2014.py")).read()
-    keep = {"winsorize", "get_subsets", "build_table_2", "create_figure_1"}
+    keep = {"winsorize", "get_subsets", "build_table_1", "build_table_2", "create_figure_1"}
     fns = [n for n in ast.parse(src).body if isinstance(n, ast.FunctionDef) and n.name in keep]
     ns = dict(np=np, pd=pd, sm=sm_obj, OUTPUT_DIR=None, Union=__import__("typing").Union,
               Path=__import__("pathlib").Path, plt=plt_obj,
@@ -270,6 +270,22 @@ def gen_nw():
     json.dump(out, open(os.path.join(HERE, "nw.json"), "w"))
 
 
+def gen_table1():
+    """build_table_1 (src/calc_Lewellen_2014.py:577-670) on the winsorize panel, whose
+    inf values survive winsorizing (NaN cuts) and exercise the inf->NaN replacement."""
+    df = cases.wins_panel()
+    ns = load_calc(RecordingPlt(), sm)
+    w = ns["winsorize"](df, cases.WINSOR_VARS, 1, 99)
+    subsets = ns["get_subsets"](w)
+    vd = dict(cases.VARIABLES_DICT)
+    vd["Missing column"] = "not_a_column"
+    t1 = ns["build_table_1"](subsets, vd)
+    meta = {"index": list(t1.index), "columns": [list(c) for c in t1.columns],
+            "values": [[None if pd.isna(x) else float(x) for x in row] for row in t1.values.tolist()],
+            "dtypes": [str(t) for t in t1.dtypes]}
+    json.dump(meta, open(os.path.join(HERE, "table1.json"), "w"), indent=1)
+
+
 def gen_pct():
     arrs = cases.percentile_arrays()
     qs = [1, 99, 20, 50, 0, 100, 37.5]
@@ -295,4 +311,5 @@ if __name__ == "__main__":
     gen_fm()
     gen_fig1()
     gen_mid()
+    gen_table1()
     print("ok")

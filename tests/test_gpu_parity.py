@@ -269,3 +269,18 @@ def test_pipeline_vs_oracle(E):
         assert_series_close(pred[k, pf, 1], r["pred_R2"], f"{name} pred R2")
         assert scalar_close(pmean[k, 0], r["pred_summary"][0], RTOL, 1e-12)
         assert scalar_close(ptst[k, 0], r["pred_summary"][1], RTOL, 1e-12)
+
+
+def test_table1_golden(CL):
+    g = load_json("table1.json")
+    df = frame_from(load_npz("wins.npz"), "in_")
+    subs = CL.get_subsets(CL.winsorize(df, cases.WINSOR_VARS, 1, 99))
+    vd = dict(cases.VARIABLES_DICT)
+    vd["Missing column"] = "not_a_column"
+    t1 = CL.build_table_1(subs, vd)
+    assert list(t1.index) == g["index"]
+    assert [list(c) for c in t1.columns] == g["columns"]
+    assert [str(t) for t in t1.dtypes] == g["dtypes"]
+    for r, row in enumerate(g["values"]):
+        for c, v in enumerate(row):
+            assert scalar_close(t1.values[r, c], v, 1e-12), (g["index"][r], g["columns"][c])
