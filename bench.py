@@ -62,6 +62,8 @@ def main():
     T_loc, N = args.months, args.firms
     T_glob = T_loc * world
     panel = E.panel_synthetic(T_loc, N, args.seed, month0=rank * T_loc, device=dev)
+    # chunk the Gram by the GLOBAL panel so per-month sums are identical for any rank count
+    panel.chunk_rows = E.default_chunk_rows(T_glob * N, T_glob, N)
     rows_local = T_loc * N
     seg_lo, seg_hi = rank * T_loc, (rank + 1) * T_loc
     counts = [T_loc] * world

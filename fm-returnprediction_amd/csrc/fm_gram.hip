@@ -17,7 +17,7 @@
 //      z[row l>>4][col l&15]), accumulating Z^T Z per bucket in registers (16x16 FP64
 //      tile = 4 doubles per lane; two tiles wide for up to 31 columns).
 // At chunk end the four waves' accumulators are summed through LDS and written as one
-// zw*zw Gram per (chunk, bucket).  fm_solve combines buckets into problems: model m's
+// packed upper-triangular Gram per (chunk, bucket).  fm_solve combines buckets into problems: model m's
 // Gram is the sum over patterns that contain m and levels >= the problem's universe,
 // restricted to m's columns.  One HBM read of the panel serves every model x universe.
 #include <math.h>
@@ -231,9 +231,11 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         }
     }
 
-    // ---- cross-wave reduction and store: partial[chunk][bucket][ZW][ZW]
+    // ---- cross-wave reduction and store: partial[chunk][bucket][packed upper triangle]
+    // (ZW*(ZW+1)/2 doubles per bucket: Z'Z is symmetric, half the bytes of a full tile)
+    constexpr int PK = ZW * (ZW + 1) / 2;
     const int nbr = a.npatterns * nlevels;
-    double* outp = a.partial + (int64_t)chunk * nbr * ZW * ZW;
+    double* outp = a.partial + (int64_t)chunk * nbr * PK;
     const int col = lane & 15, sub = lane >> 4;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -250,11 +252,19 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             }
         }
         __syncthreads();
-        for (int e = tid; e < ZW * ZW; e += GT) {
-            double s = tile[e];
+        for (int e = tid; e < PK; e += GT) {
+            // packed index e -> (i, j), i <= j, row-major over the upper triangle
+            int i = 0, rem = e;
+            while (rem >= ZW - i) {
+                rem -= ZW - i;
+                ++i;
+            }
+            const int j = i + rem;
+            const int f = i * ZW + j;
+            double s = tile[f];
 #pragma unroll
-            for (int ww = 1; ww < GNW; ++ww) s += tile[ww * ZW * ZW + e];
-            outp[(int64_t)b * ZW * ZW + e] = s;
+            for (int ww = 1; ww < GNW; ++ww) s += tile[ww * ZW * ZW + f];
+            outp[(int64_t)b * PK + e] = s;
         }
         __syncthreads();
     }

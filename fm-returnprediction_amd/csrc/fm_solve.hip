@@ -95,11 +95,11 @@ __device__ void jacobi_pinv(double* A, double* V, int K, const double* sxy, doub
 
 template <int MD>
 __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
-    extern __shared__ double bs[];                 // [nb][zw*zw] bucket sums of this month
+    extern __shared__ double bs[];   // [nb][zw(zw+1)/2] packed bucket sums of this month
     __shared__ WaveScratch<MD> ws_all[VNW];
     const int s = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-    const int zw = a.zw, zz = zw * zw;
+    const int zw = a.zw, zz = zw * (zw + 1) / 2;   // packed upper triangle per bucket
     const int nb = a.npatterns * a.nlevels;
     const int c0 = a.seg_chunk_off[s], c1 = a.seg_chunk_off[s + 1];
     for (int e = tid; e < nb * zz; e += VT) {
@@ -117,7 +117,8 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
         // ---- assemble the problem Gram G[i][j] over its buckets
         for (int e = lane; e < nz * nz; e += WAVE) {
             const int i = e / nz, j = e - (e / nz) * nz;
-            const int off = zi[i] * zw + zi[j];
+            const int zr = zi[i] < zi[j] ? zi[i] : zi[j], zc = zi[i] < zi[j] ? zi[j] : zi[i];
+            const int off = zr * zw - (zr * (zr - 1)) / 2 + (zc - zr);
             double acc = 0.0;
             for (int b = 0; b < nb; ++b) {
                 const int pid = b / a.nlevels, lvl = b - pid * a.nlevels;
@@ -400,12 +401,12 @@ extern "C" int fm_solve(const fm_solve_args* args, void* stream) {
                    a.prob_z && a.prob_nz && a.prob_flags && a.rec && a.status,
                "fm_solve: null pointer");
     FM_REQUIRE(a.zw == 16 || a.zw == 32, "fm_solve: zw must be 16 or 32");
-    FM_REQUIRE(a.npatterns * a.nlevels * a.zw * a.zw <= MAXB_LDS,
-               "fm_solve: %d buckets x %d^2 exceed the LDS budget", a.npatterns * a.nlevels, a.zw);
+    FM_REQUIRE(a.npatterns * a.nlevels * (a.zw * (a.zw + 1) / 2) <= MAXB_LDS,
+               "fm_solve: %d buckets of a %d-wide Gram exceed the LDS budget", a.npatterns * a.nlevels, a.zw);
     FM_REQUIRE(a.pmax >= 2 && a.pmax <= 32, "fm_solve: pmax must be 2..32");
     FM_REQUIRE(a.moments == nullptr || a.mom_stride > 0, "fm_solve: bad mom_stride");
     if (a.nseg == 0 || a.nprob == 0) return FM_OK;
-    const size_t dyn = (size_t)a.npatterns * a.nlevels * a.zw * a.zw * sizeof(double);
+    const size_t dyn = (size_t)a.npatterns * a.nlevels * (a.zw * (a.zw + 1) / 2) * sizeof(double);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)solve_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,

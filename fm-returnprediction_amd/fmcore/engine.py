@@ -95,6 +95,7 @@ class DevicePanel:
     me: Optional[torch.Tensor] = None  # [n] float64
     nyse: Optional[torch.Tensor] = None  # [n] uint8
     order: Optional[np.ndarray] = None   # sorted row -> original positional row
+    chunk_rows: Optional[int] = None     # Gram chunking override (sharded runs: global policy)
 
     @property
     def nrows(self):
@@ -320,17 +321,29 @@ def group_models(models: Sequence[Model], nlevels, cap):
     return groups
 
 
-def make_chunks(seg_off_h, target_chunks=2048, min_rows=512):
-    n = int(seg_off_h[-1])
+def default_chunk_rows(total_rows, nseg, max_seg_len, target_chunks=2048):
+    """Rows per Gram workgroup: whole months when there are enough months to fill the chip,
+    else months split into ~target_chunks/nseg pieces.  Callers that shard months across
+    ranks pass the GLOBAL sizes so every rank chunks (and sums) identically."""
+    if nseg == 0:
+        return 256
+    per = max(1, -(-target_chunks // nseg))
+    ch = -(-max(int(max_seg_len), 1) // per)
+    return max(256, ((ch + 255) // 256) * 256)
+
+
+def make_chunks(seg_off_h, chunk_rows):
+    """Split every month into ceil(L / chunk_rows) near-equal chunks (depends only on the
+    month's own length, so per-month arithmetic is independent of sharding)."""
     T = len(seg_off_h) - 1
-    ch = max(min_rows, -(-n // max(target_chunks, 1)))
-    ch = ((ch + 255) // 256) * 256
-    lens = np.diff(seg_off_h)
-    nch = np.maximum(1, -(-lens // ch)).astype(np.int64)
+    lens = np.diff(seg_off_h).astype(np.int64)
+    nch = np.maximum(1, -(-lens // chunk_rows)).astype(np.int64)
     seg = np.repeat(np.arange(T, dtype=np.int32), nch)
     k = np.arange(len(seg)) - np.repeat(np.cumsum(nch) - nch, nch)
-    r0 = seg_off_h[seg] + k * ch
-    r1 = np.minimum(r0 + ch, seg_off_h[seg + 1])
+    L = lens[seg]
+    n = nch[seg]
+    r0 = seg_off_h[seg] + (k * L) // n
+    r1 = seg_off_h[seg] + ((k + 1) * L) // n
     rows = np.stack([r0, r1], axis=1).reshape(-1).astype(np.int64)
     off = np.zeros(T + 1, dtype=np.int32)
     np.cumsum(nch, out=off[1:])
@@ -349,7 +362,8 @@ def _chunk_plan(panel: DevicePanel):
     cache = getattr(panel, "_chunk_cache", None)
     if cache is not None:
         return cache
-    seg, rows, off = make_chunks(panel.seg_off_h)
+    ch = panel.chunk_rows or default_chunk_rows(panel.nrows, panel.nseg, panel.max_seg_len)
+    seg, rows, off = make_chunks(panel.seg_off_h, ch)
     dev = panel.cols.device
     plan = _Plan(torch.from_numpy(seg).to(dev), torch.from_numpy(rows).to(dev),
                  torch.from_numpy(off).to(dev), len(seg))
@@ -397,7 +411,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
         mm = torch.tensor([m.mask for m in gm], dtype=torch.int64).to(torch.int32).to(dev)
         ym = torch.tensor([1 << m.y for m in gm], dtype=torch.int32, device=dev)
         lut_t = torch.from_numpy(lut).to(dev)
-        partial = torch.empty((plan.nchunks, nb, zw * zw), dtype=torch.float64, device=dev)
+        partial = torch.empty((plan.nchunks, nb, zw * (zw + 1) // 2), dtype=torch.float64, device=dev)
         flags = torch.zeros((T, len(gm)), dtype=torch.int32, device=dev)
         ga = L.GramArgs(
             cols=src.data_ptr(), col_stride=src.stride(0), ncols=ncols, nseg=T,

@@ -89,7 +89,7 @@ typedef struct fm_gram_args {
     int32_t nmodels;
     const uint8_t* pattern_id;    /* [1<<nmodels] validity pattern -> id, 255 = drop row */
     int32_t npatterns;            /* buckets = npatterns * nlevels */
-    double* partial;              /* [nchunks][nbuckets][zw*zw], zw = 16 or 32 */
+    double* partial;              /* [nchunks][nbuckets][zw*(zw+1)/2] packed upper triangle, zw = 16 or 32 */
     uint32_t* flags;              /* [nseg][nmodels], OR-ed FM_ST_INF_IN_X / _Y; zeroed by caller */
 } fm_gram_args;
 

@@ -71,15 +71,20 @@ def test_plan_patterns_nested_lewellen_models():
 
 
 def test_make_chunks_cover_segments_exactly():
-    from fmcore.engine import make_chunks
+    from fmcore.engine import default_chunk_rows, make_chunks
     seg_off = np.array([0, 0, 5000, 5003, 20000, 20001], dtype=np.int64)
-    seg, rows, off = make_chunks(seg_off, target_chunks=8, min_rows=512)
+    ch = default_chunk_rows(20001, 5, 15000, target_chunks=8)
+    seg, rows, off = make_chunks(seg_off, ch)
     rows = rows.reshape(-1, 2)
     for s in range(len(seg_off) - 1):
         mine = rows[off[s]:off[s + 1]]
         assert (seg[off[s]:off[s + 1]] == s).all()
         assert mine[0, 0] == seg_off[s] and mine[-1, 1] == seg_off[s + 1]
         assert (mine[1:, 0] == mine[:-1, 1]).all()
+        assert (mine[:, 1] - mine[:, 0] <= ch).all()
+    # a month is chunked the same way whatever else is in the panel (shard independence)
+    s2, r2, o2 = make_chunks(seg_off[2:5] - seg_off[2], ch)
+    assert np.array_equal(r2.reshape(-1, 2) + seg_off[2], rows.reshape(-1, 2)[off[2]:off[4]])
 
 
 def test_shard_bounds_balanced_and_contiguous():
