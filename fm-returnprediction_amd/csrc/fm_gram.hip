@@ -33,6 +33,8 @@ constexpr int GNW = GT / WAVE;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+__device__ const uint8_t g_zero_level[1] = {0};
+
 template <int NT, int NB, int MINW, bool PF>
 __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     constexpr int ZW = 16 * NT;
@@ -82,30 +84,25 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     }
     uint32_t fl = 0;   // bit 2m: inf in a regressor of model m; bit 2m+1: inf in its y
 
-    // Software pipeline: the next tile's loads are issued before this tile's sort and
-    // MFMA work.  Loads are unconditional (row and column clamped in range, results masked
-    // after): a load under a runtime condition makes hipcc wait vmcnt(0) per load.
-    double xv[ZW - 1];
-    {
-        const int64_t lrow = r0 + tid < r1 ? r0 + tid : r1 - 1;
+    // Software pipeline, two register buffers: tile t+1's loads are issued before tile t
+    // is sorted and accumulated (no copy between buffers, which would force vmcnt(0)).
+    // Loads are unconditional (row and column clamped in range, results masked after): a
+    // load under a runtime condition makes hipcc wait vmcnt(0) per load.
+    const uint8_t* lvbase = a.level ? a.level : g_zero_level;
+    const int64_t lvmask = a.level ? ~(int64_t)0 : 0;   // address select, not a conditional load
+    auto load_tile = [&](double (&xv)[ZW - 1], int& lv, int64_t t0) {
+        const int64_t lrow = t0 + tid < r1 ? t0 + tid : r1 - 1;
 #pragma unroll
         for (int c = 0; c < ZW - 1; ++c) {
             const int cc = c < ncols ? c : ncols - 1;
             xv[c] = a.cols[(int64_t)cc * a.col_stride + lrow];
         }
-    }
-    for (int64_t t0 = r0; t0 < r1; t0 += GT) {
+        lv = lvbase[lrow & lvmask];
+    };
+    const int col = lane & 15, sub = lane >> 4;
+    auto process_tile = [&](double (&xv)[ZW - 1], int lvraw, int64_t t0) {
         const int64_t row = t0 + tid;
         const bool inr = row < r1;
-        double xn[ZW - 1];
-        if (PF) {
-            const int64_t nrow = t0 + GT + tid < r1 ? t0 + GT + tid : r1 - 1;
-#pragma unroll
-            for (int c = 0; c < ZW - 1; ++c) {
-                const int cc = c < ncols ? c : ncols - 1;
-                xn[c] = a.cols[(int64_t)cc * a.col_stride + nrow];
-            }
-        }
         uint32_t nn = 0, infb = 0;
 #pragma unroll
         for (int c = 0; c < ZW - 1; ++c) {
@@ -124,8 +121,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         const int pid = inr ? (int)lut[pat] : 255;
         int bucket = -1;
         if (pid != 255) {
-            int lvl = a.level ? (int)a.level[row] : 0;
-            lvl = lvl < nlevels ? lvl : nlevels - 1;
+            const int lvl = lvraw < nlevels ? lvraw : nlevels - 1;
             bucket = pid * nlevels + lvl;
         }
         if (infb != 0 && bucket >= 0) {
@@ -190,34 +186,47 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             }
         }
         __syncthreads();
-        // ---- MFMA accumulation, one bucket at a time (static register indices)
-        const int col = lane & 15, sub = lane >> 4;
+        // ---- MFMA accumulation, one bucket at a time (static register indices); the
+        // bucket bounds live in SGPRs via readlane, one operand read ahead of each MFMA
+        const int bo = lane <= NB ? boff[lane] : 0;
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            const int g1 = boff[b + 1] >> 2;
-            for (int g = (boff[b] >> 2) + w; g < g1; g += GNW) {
-                const double* rp = tile + (4 * g + sub) * RS;
-                const double a0 = rp[col];
+            const int g0 = (__builtin_amdgcn_readlane(bo, b) >> 2) + w;
+            const int g1 = __builtin_amdgcn_readlane(bo, b + 1) >> 2;
+            if (g0 >= g1) continue;
+            const double* rp = tile + (4 * g0 + sub) * RS;
+            double a0 = rp[col];
+            double a1 = NT == 2 ? rp[16 + col] : 0.0;
+            for (int g = g0; g < g1; g += GNW) {
+                const int gn = g + GNW < g1 ? g + GNW : g;
+                const double* rn = tile + (4 * gn + sub) * RS;
+                const double n0 = rn[col];
+                const double n1 = NT == 2 ? rn[16 + col] : 0.0;
                 acc0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a0, acc0[b], 0, 0, 0);
                 if (NT == 2) {
-                    const double a1 = rp[16 + col];
                     acc1[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a1, acc1[b], 0, 0, 0);
                     acc2[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, a1, acc2[b], 0, 0, 0);
                 }
+                a0 = n0;
+                a1 = n1;
             }
         }
         __syncthreads();
-        if (PF) {
-#pragma unroll
-            for (int c = 0; c < ZW - 1; ++c) xv[c] = xn[c];
-        } else {
-            const int64_t nrow = t0 + GT + tid < r1 ? t0 + GT + tid : r1 - 1;
-#pragma unroll
-            for (int c = 0; c < ZW - 1; ++c) {
-                const int cc = c < ncols ? c : ncols - 1;
-                xv[c] = a.cols[(int64_t)cc * a.col_stride + nrow];
-            }
-        }
+    };
+
+    double xa[ZW - 1], xb[ZW - 1];
+    int la = 0, lb = 0;
+    load_tile(xa, la, r0);
+    for (int64_t t0 = r0; t0 < r1;) {
+        if (PF) load_tile(xb, lb, t0 + GT);
+        process_tile(xa, la, t0);
+        t0 += GT;
+        if (t0 >= r1) break;
+        if (!PF) load_tile(xb, lb, t0);
+        if (PF) load_tile(xa, la, t0 + GT);
+        process_tile(xb, lb, t0);
+        t0 += GT;
+        if (!PF && t0 < r1) load_tile(xa, la, t0);
     }
 
     // ---- inf flags (rare): one atomic per wave per model
@@ -236,7 +245,6 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     constexpr int PK = ZW * (ZW + 1) / 2;
     const int nbr = a.npatterns * nlevels;
     double* outp = a.partial + (int64_t)chunk * nbr * PK;
-    const int col = lane & 15, sub = lane >> 4;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         if (b >= nbr) continue;   // block-uniform
