@@ -200,6 +200,137 @@ __device__ __forceinline__ void select_ranks(uint64_t (&keys)[VPT], int n, int r
     for (int v = 0; v < VPT; ++v) keys[v] = keys[v] == SENT ? SENT : ~keys[v];
 }
 
+// Bitonic sort (ascending) of the 64*R keys held by one wave: element e = lane + 64*r lives
+// in register r of lane e&63.  Cross-lane stages exchange through ds_bpermute; the j=64
+// stage of R=2 is register-local.
+template <int R>
+__device__ __forceinline__ void wave_sort(uint64_t (&v)[R]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= WAVE * R; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= WAVE) {
+                const int rj = j / WAVE;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (r & rj) continue;
+                    const bool up = (((lane + WAVE * r) & k) == 0);
+                    const uint64_t a = v[r], b = v[r | rj];
+                    const uint64_t mn = a < b ? a : b, mx = a < b ? b : a;
+                    v[r] = up ? mn : mx;
+                    v[r | rj] = up ? mx : mn;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint64_t p = (uint64_t)__shfl_xor((long long)v[r], j, WAVE);
+                    const bool up = (((lane + WAVE * r) & k) == 0);
+                    const bool lower = (lane & j) == 0;
+                    const bool take_min = lower == up;
+                    const uint64_t mn = p < v[r] ? p : v[r], mx = p < v[r] ? v[r] : p;
+                    v[r] = take_min ? mn : mx;
+                }
+            }
+        }
+    }
+}
+
+// Sort buf[0..c) (c <= 64*R) in place with one wave; entries c..64R-1 become SENT.
+template <int R>
+__device__ __forceinline__ void wave_sort_lds(uint64_t* buf, int c) {
+    const int lane = lane_id();
+    uint64_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane + WAVE * r;
+        v[r] = e < c ? buf[e] : SENT;
+    }
+    wave_sort<R>(v);
+#pragma unroll
+    for (int r = 0; r < R; ++r) buf[lane + WAVE * r] = v[r];
+}
+
+// Both winsorize tails at once: keys at ranks li <= lj (lower tail) and hi_i <= hi_j (upper
+// tail), n valid keys.  Returns false (nothing written, block-uniform) when the fast path
+// does not apply; the caller then uses select_ranks.
+//   tau_lo = max over the 4 waves of the wave's k-th smallest thread minimum,
+//   k = ceil((lj+1)/4): 4k >= lj+1 distinct keys are <= tau_lo, so s[lj] <= tau_lo, and
+//   only the keys < tau_lo (about lj of them) can precede it.  Same for the upper tail on
+//   complemented keys.  Candidates are compacted with one packed scan and sorted by one
+//   wave per tail.
+template <int VPT>
+__device__ __forceinline__ bool select_tails(const uint64_t (&keys)[VPT], int n, int li, int lj,
+                                             int hi_i, int hi_j, uint64_t& k0, uint64_t& k1,
+                                             uint64_t& k2, uint64_t& k3, SelSmem& sm) {
+    const int ci = n - 1 - hi_j, cj = n - 1 - hi_i;   // upper-tail ranks in complemented order
+    if (lj >= ST - 3 || cj >= ST - 3) return false;
+    uint64_t mn = SENT, cmn = SENT;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const uint64_t k = keys[v];
+        const uint64_t ck = k == SENT ? SENT : ~k;
+        mn = k < mn ? k : mn;
+        cmn = ck < cmn ? ck : cmn;
+    }
+    uint64_t a[1] = {mn}, b[1] = {cmn};
+    wave_sort<1>(a);
+    wave_sort<1>(b);
+    const int w = threadIdx.x / WAVE, lane = lane_id();
+    const int klo = (lj + 4) / 4, khi = (cj + 4) / 4;
+    __syncthreads();   // sm.bc / sm.buf may still be read by a previous phase
+    if (lane == klo - 1) sm.buf[CAND_CAP - 8 + w] = a[0];
+    if (lane == khi - 1) sm.buf[CAND_CAP - 4 + w] = b[0];
+    __syncthreads();
+    uint64_t tlo = 0, thi = 0;
+#pragma unroll
+    for (int i = 0; i < SNW; ++i) {
+        const uint64_t x = sm.buf[CAND_CAP - 8 + i], y = sm.buf[CAND_CAP - 4 + i];
+        tlo = x > tlo ? x : tlo;
+        thi = y > thi ? y : thi;
+    }
+    if (tlo == SENT || thi == SENT) return false;   // some wave lacks k valid thread minima
+    int cnt = 0;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const uint64_t k = keys[v];
+        const uint64_t ck = k == SENT ? SENT : ~k;
+        cnt += (k < tlo ? 1 : 0) + (ck < thi ? 0x10000 : 0);
+    }
+    int tot = 0;
+    const int off = block_excl_scan<SNW>(cnt, sm.ints, &tot);
+    const int clo = tot & 0xFFFF, chi = tot >> 16;
+    constexpr int HALF = CAND_CAP / 2;
+    if (clo > 2 * WAVE || chi > 2 * WAVE) return false;   // block-uniform
+    {
+        int ol = off & 0xFFFF, oh = HALF + (off >> 16);
+        __syncthreads();
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            const uint64_t k = keys[v];
+            const uint64_t ck = k == SENT ? SENT : ~k;
+            if (k < tlo) sm.buf[ol++] = k;
+            if (ck < thi) sm.buf[oh++] = ck;
+        }
+        __syncthreads();
+    }
+    if (w == 0) {
+        if (clo <= WAVE) wave_sort_lds<1>(sm.buf, clo);
+        else wave_sort_lds<2>(sm.buf, clo);
+    } else if (w == 1) {
+        if (chi <= WAVE) wave_sort_lds<1>(sm.buf + HALF, chi);
+        else wave_sort_lds<2>(sm.buf + HALF, chi);
+    }
+    __syncthreads();
+    k0 = li < clo ? sm.buf[li] : tlo;
+    k1 = lj < clo ? sm.buf[lj] : tlo;
+    const uint64_t ca = ci < chi ? sm.buf[HALF + ci] : thi;
+    const uint64_t cb = cj < chi ? sm.buf[HALF + cj] : thi;
+    k3 = ~ca;   // rank hi_j (complemented rank ci)
+    k2 = ~cb;   // rank hi_i
+    return true;
+}
+
 // numpy 'linear' (mode 0, function_base._quantile/_lerp) or pandas group_quantile (mode 1)
 __device__ __forceinline__ void qranks(int n, double q, int mode, int& i, int& j, double& g) {
     if (mode == 0) {
@@ -273,8 +404,10 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
         qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
         uint64_t k0, k1, k2, k3;
-        select_ranks<VPT>(keys, n, i0, j0, k0, k1, sm);
-        select_ranks<VPT>(keys, n, i1, j1, k2, k3, sm);
+        if (!select_tails<VPT>(keys, n, i0, j0, i1, j1, k0, k1, k2, k3, sm)) {
+            select_ranks<VPT>(keys, n, i0, j0, k0, k1, sm);
+            select_ranks<VPT>(keys, n, i1, j1, k2, k3, sm);
+        }
         lo = qlerp(kval(k0), kval(k1), g0, a.lerp_mode);
         hi = qlerp(kval(k2), kval(k3), g1, a.lerp_mode);
     }

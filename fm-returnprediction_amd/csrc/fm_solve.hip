@@ -24,6 +24,7 @@ namespace {
 constexpr int VT = 256;
 constexpr int VNW = VT / WAVE;
 constexpr int MAXB_LDS = 8192;   // doubles of bucket sums held in LDS (64 KB max)
+constexpr int64_t SCAN_GRID = 1024;   // workgroups of the status-scanning fix-up launches
 constexpr double CHOL_REL = 1e-9;
 constexpr double EIG_REL = 1e-12;
 
@@ -244,9 +245,21 @@ __global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t s
                                                    const uint8_t* level, int nprob,
                                                    const int32_t* prob_level, const int32_t* prob_z,
                                                    const int32_t* prob_nz, const int32_t* pairs,
-                                                   uint32_t* status) {
+                                                   int npairs, uint32_t* status) {
     __shared__ uint64_t red[VNW];
-    const int s = pairs[2 * blockIdx.x], p = pairs[2 * blockIdx.x + 1];
+    // npairs < 0: scan every (month, problem) and take those the solve flagged, so the
+    // check needs no host round trip; else the listed pairs.
+    const int total = npairs < 0 ? nseg * nprob : npairs;
+    for (int e = blockIdx.x; e < total; e += gridDim.x) {
+    int s, p;
+    if (npairs < 0) {
+        s = e / nprob;
+        p = e - s * nprob;
+        if (!(status[e] & FM_ST_CONST_SUSPECT)) continue;
+    } else {
+        s = pairs[2 * e];
+        p = pairs[2 * e + 1];
+    }
     const int nz = prob_nz[p], K = nz - 2, u = prob_level[p];
     const int* zi = prob_z + p * 32;
     const int64_t r0 = seg_off[s], r1 = seg_off[s + 1];
@@ -282,6 +295,7 @@ __global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t s
         if (kmin != SENT && kmin == kmax && nzr == 0) any_const = true;
     }
     if (threadIdx.x == 0 && any_const) status[(int64_t)s * nprob + p] |= FM_ST_CONST_COL;
+    }
 }
 
 // inf in y (statsmodels keeps the month): params = pinv(X) @ y, so each coefficient is the
@@ -289,20 +303,26 @@ __global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t s
 // result is +inf, -inf or NaN (mixed signs, or 0*inf).  pinv[:,i] for the slopes is
 // Sxx^{-1}(x_i - xbar) and for the intercept 1/n - xbar'Sxx^{-1}(x_i - xbar).  One
 // workgroup per flagged (month, problem); R^2 becomes NaN as in statsmodels.
-__global__ __launch_bounds__(VT) void infy_kernel(const double* cols, int64_t stride,
-                                                  const int64_t* seg_off, int nseg, const double* lo,
-                                                  const double* hi, const double* shift,
-                                                  const double* inv_scale, const double* add_back,
-                                                  const uint8_t* level, int nprob,
-                                                  const int32_t* prob_level, const int32_t* prob_z,
-                                                  const int32_t* prob_nz, const int32_t* pairs,
-                                                  const double* moments, int mom_stride, int pmax,
-                                                  double* rec, uint32_t* status) {
-    __shared__ double Lm[32 * 32];
-    __shared__ double mu[32], xb[32];
-    __shared__ unsigned bits[32];
-    __shared__ int okf;
-    const int s = pairs[2 * blockIdx.x], p = pairs[2 * blockIdx.x + 1];
+struct InfySmem {
+    double Lm[32 * 32];
+    double mu[32], xb[32];
+    unsigned bits[32];
+    int okf;
+};
+
+__device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, const double* cols, int64_t stride,
+                                          const int64_t* seg_off, int nseg, const double* lo,
+                                          const double* hi, const double* shift,
+                                          const double* inv_scale, const double* add_back,
+                                          const uint8_t* level, int nprob,
+                                          const int32_t* prob_level, const int32_t* prob_z,
+                                          const int32_t* prob_nz, const double* moments,
+                                          int mom_stride, int pmax, double* rec) {
+    double* Lm = sm.Lm;
+    double* mu = sm.mu;
+    double* xb = sm.xb;
+    unsigned* bits = sm.bits;
+    int& okf = sm.okf;
     const int nz = prob_nz[p], K = nz - 2, K1 = K + 1, u = prob_level[p];
     const int* zi = prob_z + p * 32;
     const double* mo = moments + ((int64_t)s * nprob + p) * mom_stride;
@@ -390,6 +410,35 @@ __global__ __launch_bounds__(VT) void infy_kernel(const double* cols, int64_t st
     if (threadIdx.x == 0) rec[ro + pmax] = NAN;
 }
 
+__global__ __launch_bounds__(VT) void infy_kernel(const double* cols, int64_t stride,
+                                                  const int64_t* seg_off, int nseg, const double* lo,
+                                                  const double* hi, const double* shift,
+                                                  const double* inv_scale, const double* add_back,
+                                                  const uint8_t* level, int nprob,
+                                                  const int32_t* prob_level, const int32_t* prob_z,
+                                                  const int32_t* prob_nz, const int32_t* pairs,
+                                                  int npairs, const double* moments, int mom_stride,
+                                                  int pmax, double* rec, const uint32_t* status) {
+    __shared__ InfySmem sm;
+    // npairs < 0: scan every (month, problem) for FITTED|INF_IN_Y (no host round trip)
+    const int total = npairs < 0 ? nseg * nprob : npairs;
+    for (int e = blockIdx.x; e < total; e += gridDim.x) {
+        int s, p;
+        if (npairs < 0) {
+            const uint32_t st = status[e];
+            if (!(st & FM_ST_FITTED) || !(st & FM_ST_INF_IN_Y)) continue;
+            s = e / nprob;
+            p = e - s * nprob;
+        } else {
+            s = pairs[2 * e];
+            p = pairs[2 * e + 1];
+        }
+        infy_pair(s, p, sm, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level,
+                  nprob, prob_level, prob_z, prob_nz, moments, mom_stride, pmax, rec);
+        __syncthreads();   // sm is reused by the next pair
+    }
+}
+
 }  // namespace
 }  // namespace fm
 
@@ -430,13 +479,15 @@ extern "C" int fm_const_check(const double* cols, int64_t col_stride, int32_t nc
                               const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
                               uint32_t* status, void* stream) {
     using namespace fm;
-    FM_REQUIRE(cols && seg_off && prob_level && prob_z && prob_nz && pairs && status,
-               "fm_const_check: null pointer");
+    FM_REQUIRE(cols && seg_off && prob_level && prob_z && prob_nz && status &&
+                   (pairs || npairs < 0), "fm_const_check: null pointer");
     FM_REQUIRE((lo == nullptr) == (hi == nullptr), "fm_const_check: lo/hi must both be set or NULL");
-    if (npairs == 0) return FM_OK;
-    hipLaunchKernelGGL(const_kernel, dim3(npairs), dim3(VT), 0, (hipStream_t)stream, cols,
+    const int64_t work = npairs < 0 ? (int64_t)nseg * nprob : npairs;
+    if (work == 0) return FM_OK;
+    const int grid = (int)(npairs < 0 ? (work < SCAN_GRID ? work : SCAN_GRID) : work);
+    hipLaunchKernelGGL(const_kernel, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols,
                        col_stride, ncols, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
-                       prob_nz, pairs, status);
+                       prob_nz, pairs, npairs, status);
     FM_CHECK_LAUNCH("fm_const_check");
     return FM_OK;
 }
@@ -449,13 +500,15 @@ extern "C" int fm_inf_y_fix(const double* cols, int64_t col_stride, const int64_
                             const double* moments, int32_t mom_stride, int32_t pmax, double* rec,
                             uint32_t* status, void* stream) {
     using namespace fm;
-    FM_REQUIRE(cols && seg_off && prob_level && prob_z && prob_nz && pairs && moments && rec && status,
-               "fm_inf_y_fix: null pointer");
+    FM_REQUIRE(cols && seg_off && prob_level && prob_z && prob_nz && moments && rec && status &&
+                   (pairs || npairs < 0), "fm_inf_y_fix: null pointer");
     FM_REQUIRE((lo == nullptr) == (hi == nullptr), "fm_inf_y_fix: lo/hi must both be set or NULL");
-    if (npairs == 0) return FM_OK;
-    hipLaunchKernelGGL(infy_kernel, dim3(npairs), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
+    const int64_t work = npairs < 0 ? (int64_t)nseg * nprob : npairs;
+    if (work == 0) return FM_OK;
+    const int grid = (int)(npairs < 0 ? (work < SCAN_GRID ? work : SCAN_GRID) : work);
+    hipLaunchKernelGGL(infy_kernel, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
                        seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
-                       prob_z, prob_nz, pairs, moments, mom_stride, pmax, rec, status);
+                       prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status);
     FM_CHECK_LAUNCH("fm_inf_y_fix");
     return FM_OK;
 }

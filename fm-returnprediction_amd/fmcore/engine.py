@@ -371,6 +371,60 @@ def _chunk_plan(panel: DevicePanel):
     return plan
 
 
+@dataclass
+class _GroupPlan:
+    """Device-resident description of one model group (built once per model set)."""
+    nmodels: int
+    npatterns: int
+    nprob: int
+    mm: torch.Tensor     # [nmodels] column masks
+    ym: torch.Tensor     # [nmodels] y-column bit
+    lut: torch.Tensor    # [1<<nmodels] validity pattern -> pattern index
+    patm: torch.Tensor   # [npatterns] model set of each pattern
+    pm: torch.Tensor     # [nprob] group-local model of each problem
+    pl: torch.Tensor     # [nprob] universe level
+    pf: torch.Tensor     # [nprob] const-check flag
+    pz: torch.Tensor     # [nprob, 32] z columns (0 = intercept, 1+c = panel column c)
+    pnz: torch.Tensor    # [nprob]
+    idx: torch.Tensor    # [nprob] global problem index
+
+
+def _group_plans(panel, models, problems, nlevels, cap, const_check, dev):
+    key = (tuple((m.y, tuple(m.xs), tuple(m.levels), bool(m.const_check)) for m in models),
+           nlevels, cap, bool(const_check), str(dev))
+    cache = panel.__dict__.setdefault("_group_cache", {})
+    if key in cache:
+        return cache[key]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    plans = []
+    for g in group_models(models, nlevels, cap):
+        gm = [models[i] for i in g]
+        lut, pats = plan_patterns(gm)
+        gp = [(k, p) for k, p in enumerate(problems) if p.model in g]
+        local = {mi: j for j, mi in enumerate(g)}
+        pz = np.zeros((len(gp), 32), dtype=np.int32)
+        pnz = np.zeros(len(gp), dtype=np.int32)
+        for j, (_, p) in enumerate(gp):
+            m = models[p.model]
+            z = [0] + [1 + x for x in m.xs] + [1 + m.y]
+            pz[j, :len(z)] = z
+            pnz[j] = len(z)
+        plans.append(_GroupPlan(
+            nmodels=len(gm), npatterns=len(pats), nprob=len(gp),
+            mm=t(np.array([m.mask for m in gm], dtype=np.int64).astype(np.int32)),
+            ym=t(np.array([1 << m.y for m in gm], dtype=np.int32)),
+            lut=t(lut),
+            patm=t(np.array(pats, dtype=np.int64).astype(np.uint32).view(np.int32)),
+            pm=t(np.array([local[p.model] for _, p in gp], dtype=np.int32)),
+            pl=t(np.array([p.level for _, p in gp], dtype=np.int32)),
+            pf=t(np.array([1 if (models[p.model].const_check and const_check) else 0 for _, p in gp],
+                          dtype=np.int32)),
+            pz=t(pz), pnz=t(pnz),
+            idx=t(np.array([k for k, _ in gp], dtype=np.int64))))
+    cache[key] = plans
+    return plans
+
+
 def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, cuts: Cuts = None,
             shift=None, inv_scale=None, add_back=None, moments=False, cols=None, const_check=True):
     """One batched cross-sectional pass: every (model, universe level) problem for every
@@ -403,84 +457,52 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
     plan = _chunk_plan(panel)
     lo = cuts.lo if cuts is not None else None
     hi = cuts.hi if cuts is not None else None
-    groups = group_models(models, nlevels, cap)
-    for g in groups:
-        gm = [models[i] for i in g]
-        lut, pats = plan_patterns(gm)
-        nb = len(pats) * nlevels
-        mm = torch.tensor([m.mask for m in gm], dtype=torch.int64).to(torch.int32).to(dev)
-        ym = torch.tensor([1 << m.y for m in gm], dtype=torch.int32, device=dev)
-        lut_t = torch.from_numpy(lut).to(dev)
+    groups = _group_plans(panel, models, problems, nlevels, cap, const_check, dev)
+    for gpl in groups:
+        nb = gpl.npatterns * nlevels
         partial = torch.empty((plan.nchunks, nb, zw * (zw + 1) // 2), dtype=torch.float64, device=dev)
-        flags = torch.zeros((T, len(gm)), dtype=torch.int32, device=dev)
+        flags = torch.zeros((T, gpl.nmodels), dtype=torch.int32, device=dev)
         ga = L.GramArgs(
             cols=src.data_ptr(), col_stride=src.stride(0), ncols=ncols, nseg=T,
             seg_off=panel.seg_off.data_ptr(), chunk_seg=plan.chunk_seg.data_ptr(),
             chunk_row=plan.chunk_row.data_ptr(), nchunks=plan.nchunks,
             lo=_ptr(lo), hi=_ptr(hi), shift=_ptr(shift), inv_scale=_ptr(inv_scale),
-            level=_ptr(level), nlevels=nlevels, model_mask=mm.data_ptr(), model_ymask=ym.data_ptr(),
-            nmodels=len(gm), pattern_id=lut_t.data_ptr(), npatterns=len(pats),
-            partial=partial.data_ptr(), flags=flags.data_ptr())
+            level=_ptr(level), nlevels=nlevels, model_mask=gpl.mm.data_ptr(),
+            model_ymask=gpl.ym.data_ptr(), nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(),
+            npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr())
         _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
-        gp = [(k, p) for k, p in enumerate(problems) if p.model in g]
-        local = {mi: j for j, mi in enumerate(g)}
-        pz = np.zeros((len(gp), 32), dtype=np.int32)
-        pnz = np.zeros(len(gp), dtype=np.int32)
-        for j, (_, p) in enumerate(gp):
-            m = models[p.model]
-            z = [0] + [1 + x for x in m.xs] + [1 + m.y]
-            pz[j, :len(z)] = z
-            pnz[j] = len(z)
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-        pm = t(np.array([local[p.model] for _, p in gp], dtype=np.int32))
-        pl = t(np.array([p.level for _, p in gp], dtype=np.int32))
-        pf = t(np.array([1 if (models[p.model].const_check and const_check) else 0 for _, p in gp],
-                        dtype=np.int32))
-        pzt, pnzt = t(pz), t(pnz)
-        patm = t(np.array(pats, dtype=np.int64).astype(np.uint32).view(np.int32))
-        grec = torch.empty((T, len(gp), rs), dtype=torch.float64, device=dev)
-        gst = torch.zeros((T, len(gp)), dtype=torch.int32, device=dev)
+        ng = gpl.nprob
+        grec = torch.empty((T, ng, rs), dtype=torch.float64, device=dev)
+        gst = torch.empty((T, ng), dtype=torch.int32, device=dev)   # the solve writes every entry
         # centered moments are always produced: the inf-in-y fix reads them
-        gmom = torch.empty((T, len(gp), mom_stride), dtype=torch.float64, device=dev)
+        gmom = torch.empty((T, ng, mom_stride), dtype=torch.float64, device=dev)
         sa = L.SolveArgs(
             partial=partial.data_ptr(), seg_chunk_off=plan.seg_chunk_off.data_ptr(), nseg=T, zw=zw,
-            nlevels=nlevels, npatterns=len(pats), pattern_models=patm.data_ptr(), nprob=len(gp),
-            prob_model=pm.data_ptr(), prob_level=pl.data_ptr(), prob_z=pzt.data_ptr(),
-            prob_nz=pnzt.data_ptr(), prob_flags=pf.data_ptr(), add_back=_ptr(add_back),
-            gram_flags=flags.data_ptr(), nmodels=len(gm), pmax=pmax, rec=grec.data_ptr(),
+            nlevels=nlevels, npatterns=gpl.npatterns, pattern_models=gpl.patm.data_ptr(), nprob=ng,
+            prob_model=gpl.pm.data_ptr(), prob_level=gpl.pl.data_ptr(), prob_z=gpl.pz.data_ptr(),
+            prob_nz=gpl.pnz.data_ptr(), prob_flags=gpl.pf.data_ptr(), add_back=_ptr(add_back),
+            gram_flags=flags.data_ptr(), nmodels=gpl.nmodels, pmax=pmax, rec=grec.data_ptr(),
             status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride)
         _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
-        idx = torch.tensor([k for k, _ in gp], dtype=torch.int64, device=dev)
+        # inf in y: statsmodels' pinv(X) @ y gives +-inf / NaN coefficients.  The fix-up scans
+        # the status on the device (npairs = -1), so there is no host round trip.
+        _kcall("fm_inf_y_fix", "fm_inf_y_fix", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
+               _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), ng,
+               gpl.pl.data_ptr(), gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1,
+               gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), _stream())
+        # exact nonzero-constant test where the Gram flagged a near-zero variance
+        if const_check:
+            _kcall("fm_const_check", "fm_const_check", src.data_ptr(), src.stride(0), ncols,
+                   panel.seg_off.data_ptr(), T, _ptr(lo), _ptr(hi), _ptr(level), ng, gpl.pl.data_ptr(),
+                   gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1, gst.data_ptr(), _stream())
         if len(groups) == 1:
             rec, status = grec, gst
             mom = gmom if moments else None
         else:
-            rec.index_copy_(1, idx, grec)
-            status.index_copy_(1, idx, gst)
+            rec.index_copy_(1, gpl.idx, grec)
+            status.index_copy_(1, gpl.idx, gst)
             if moments:
-                mom.index_copy_(1, idx, gmom)
-        # inf in y: statsmodels' pinv(X) @ y gives +-inf / NaN coefficients (rare; one sync)
-        iy = (((gst & L.FM_ST_FITTED) != 0) & ((gst & L.FM_ST_INF_IN_Y) != 0)).nonzero()
-        if iy.numel():
-            pairs = iy.to(torch.int32).contiguous()
-            _kcall("fm_inf_y_fix", "fm_inf_y_fix", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
-                   _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), len(gp),
-                   pl.data_ptr(), pzt.data_ptr(), pnzt.data_ptr(), pairs.data_ptr(), pairs.shape[0],
-                   gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), _stream())
-            if len(groups) > 1:
-                rec.index_copy_(1, idx, grec)
-        # exact nonzero-constant test where the Gram flagged a near-zero variance
-        if const_check:
-            sus = ((gst & L.FM_ST_CONST_SUSPECT) != 0).nonzero()
-            if sus.numel():
-                pairs = sus.to(torch.int32).contiguous()
-                _kcall("fm_const_check", "fm_const_check", src.data_ptr(), src.stride(0), ncols, panel.seg_off.data_ptr(),
-                       T, _ptr(lo), _ptr(hi), _ptr(level), len(gp), pl.data_ptr(), pzt.data_ptr(),
-                       pnzt.data_ptr(), pairs.data_ptr(), pairs.shape[0], gst.data_ptr(), _stream())
-                if len(groups) == 1:
-                    status = gst
-                else:
-                    status.index_copy_(1, idx, gst)
+                mom.index_copy_(1, gpl.idx, gmom)
     return FMResult(problems=problems, rec=rec, status=status, pmax=pmax, moments=mom,
                     mom_stride=mom_stride)
 
@@ -542,6 +564,18 @@ def rolling_result(res: FMResult, ix: TSIndex, window=120, min_periods=60):
     return out
 
 
+_SMALL = {}
+
+
+def _small_tensor(values, dtype, dev):
+    """Cached device copy of a small constant list (no per-call host-to-device copy)."""
+    key = (values, dtype, str(dev))
+    t = _SMALL.get(key)
+    if t is None:
+        t = _SMALL[key] = torch.tensor(list(values), dtype=dtype, device=dev)
+    return t
+
+
 def predictive_result(res: FMResult, ix: TSIndex, roll, lag=1, seg_lo=0, seg_hi=None, moments=None):
     """A7/A8 per (problem, fitted-month row): slope, R2, N of y on the lagged-rolling
     forecast, from the month's centered moments.  In sharded runs ``res`` holds the
@@ -550,7 +584,7 @@ def predictive_result(res: FMResult, ix: TSIndex, roll, lag=1, seg_lo=0, seg_hi=
     dev = res.rec.device
     mom = res.moments if moments is None else moments
     seg_hi = T if seg_hi is None else seg_hi
-    pk = torch.tensor([p.K for p in res.problems], dtype=torch.int32, device=dev)
+    pk = _small_tensor(tuple(p.K for p in res.problems), torch.int32, dev)
     pred = torch.empty((P, T, 4), dtype=torch.float64, device=dev)
     pst = torch.empty((P, T), dtype=torch.int32, device=dev)
     _kcall("fm_predictive", "fm_predictive", mom.data_ptr(), res.mom_stride, T, P, pk.data_ptr(),

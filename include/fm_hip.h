@@ -147,6 +147,9 @@ int fm_gram(const fm_gram_args* args, void* stream);
 
 int fm_solve(const fm_solve_args* args, void* stream);
 
+/* fm_const_check / fm_inf_y_fix: `pairs` lists (month, problem) int32 pairs; npairs < 0
+ * (pairs may be NULL) scans every pair on the device and takes those whose status bits ask
+ * for the fix-up (CONST_SUSPECT; FITTED|INF_IN_Y), so callers need no host round trip. */
 int fm_const_check(const double* cols, int64_t col_stride, int32_t ncols,
                    const int64_t* seg_off, int32_t nseg,
                    const double* lo, const double* hi, const uint8_t* level,

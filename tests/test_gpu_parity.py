@@ -56,6 +56,49 @@ def test_percentile_cuts_bit_exact(E):
         assert _same(hi, ref[:, b]), qs[b]
 
 
+def _adversarial_segments(rng):
+    """Month segments that stress the tail fast path and its fallbacks: row-sorted data
+    (the thread minima all sit in one wave), heavy ties, constants, infinities, NaNs, and
+    lengths around the 256-thread / 64-lane boundaries."""
+    segs = []
+    for n in (1, 2, 3, 5, 10, 50, 63, 64, 65, 255, 256, 257, 1000, 5000, 12345, 24000):
+        x = rng.standard_normal(n)
+        segs.append(x)
+        segs.append(np.sort(x))
+        segs.append(np.sort(x)[::-1].copy())
+        segs.append(rng.integers(0, 3, n).astype(np.float64))
+        segs.append(np.full(n, 1.5))
+        y = rng.standard_t(2, n)
+        y[rng.random(n) < 0.3] = np.nan
+        if n > 4:
+            y[:2] = [np.inf, -np.inf]
+        segs.append(y)
+        z = rng.standard_normal(n)
+        z[rng.random(n) < 0.05] = 0.0
+        z[rng.random(n) < 0.05] = -0.0
+        segs.append(z)
+    return segs
+
+
+def test_percentile_tails_adversarial(E):
+    rng = np.random.default_rng(7)
+    segs = _adversarial_segments(rng)
+    vals = np.concatenate(segs)
+    labels = np.repeat(np.arange(len(segs)), [len(s) for s in segs])
+    panel = E.panel_from_arrays([vals], ["v"], labels)
+    for qa, qb in ((1, 99), (0, 100), (0.5, 99.5), (5, 95), (25, 75), (10, 99)):
+        cuts = E.select_cuts(panel, qa / 100, qb / 100, 1, E.LERP_NUMPY)
+        lo, hi = cuts.lo.cpu().numpy()[0], cuts.hi.cpu().numpy()[0]
+        for t, s in enumerate(segs):
+            v = s[~np.isnan(s)]
+            if len(v) == 0:
+                assert np.isnan(lo[t]) and np.isnan(hi[t])
+                continue
+            with np.errstate(invalid="ignore"):
+                ra, rb = np.percentile(v, qa), np.percentile(v, qb)
+            assert _same([lo[t]], [ra]) and _same([hi[t]], [rb]), (qa, qb, t, len(v), lo[t], ra, hi[t], rb)
+
+
 def test_pandas_quantile_bit_exact(E):
     g = load_npz("pct.npz")
     vals, off, ref = g["values"], g["offsets"], g["pd_quantile"]
