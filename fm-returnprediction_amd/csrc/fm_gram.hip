@@ -33,8 +33,6 @@ constexpr int GNW = GT / WAVE;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-__device__ const uint8_t g_zero_level[1] = {0};
-
 template <int NT, int NB, int MINW, bool PF>
 __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     constexpr int ZW = 16 * NT;
@@ -52,27 +50,30 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
-    const int w = tid / WAVE;
+    const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);   // wave-uniform (SGPR loops)
     const int chunk = blockIdx.x;
     const int seg = a.chunk_seg[chunk];
     const int64_t r0 = a.chunk_row[2 * chunk], r1 = a.chunk_row[2 * chunk + 1];
     const int ncols = a.ncols, nseg = a.nseg, nmodels = a.nmodels, nlevels = a.nlevels;
 
-    for (int c = tid; c < 32; c += GT) {
-        const bool on = c < ncols;
-        const int64_t o = (int64_t)c * nseg + seg;
-        prm[0][c] = (on && a.lo) ? a.lo[o] : NAN;
-        prm[1][c] = (on && a.hi) ? a.hi[o] : NAN;
-        prm[2][c] = (on && a.shift) ? a.shift[o] : 0.0;
-        prm[3][c] = (on && a.inv_scale) ? a.inv_scale[o] : 1.0;
+    // Prologue loads are unconditional (pointer/index selected, value masked after) and are
+    // issued before the first tile, so they cost one HBM round trip, not one per load.
+    double pv;
+    int lutv, mmv, ymv;
+    {
+        const int kind = tid >> 5, c = tid & 31;
+        const double* src = kind == 0 ? a.lo : kind == 1 ? a.hi : kind == 2 ? a.shift : a.inv_scale;
+        const bool on = tid < 128 && c < ncols && src != nullptr;
+        const double* pp = on ? src + (int64_t)c * nseg + seg : a.cols;
+        const double v = *pp;
+        const double dflt = kind < 2 ? NAN : (kind == 2 ? 0.0 : 1.0);
+        pv = on ? v : dflt;
+        const int npat = 1 << nmodels;
+        lutv = a.pattern_id[tid < npat ? tid : 0];
+        const int mi = tid < nmodels ? tid : 0;
+        mmv = (int)a.model_mask[mi];
+        ymv = (int)a.model_ymask[mi];
     }
-    for (int i = tid; i < (1 << nmodels); i += GT) lut[i] = a.pattern_id[i];
-    if (tid < nmodels) {
-        mmask[tid] = a.model_mask[tid];
-        ymask[tid] = a.model_ymask[tid];
-    }
-    __syncthreads();
-
     d4 acc0[NB], acc1[NB], acc2[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -88,8 +89,12 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     // is sorted and accumulated (no copy between buffers, which would force vmcnt(0)).
     // Loads are unconditional (row and column clamped in range, results masked after): a
     // load under a runtime condition makes hipcc wait vmcnt(0) per load.
-    const uint8_t* lvbase = a.level ? a.level : g_zero_level;
+    // Without universes the level load reads byte 0 of the panel and is masked to 0.  The base
+    // must be a kernel-argument pointer: a __device__ global would make it a flat load, which
+    // also counts in lgkmcnt, so every LDS wait of the tile would wait for HBM.
+    const uint8_t* lvbase = a.level ? a.level : (const uint8_t*)a.cols;
     const int64_t lvmask = a.level ? ~(int64_t)0 : 0;   // address select, not a conditional load
+    const int lvand = a.level ? 0xFF : 0;
     auto load_tile = [&](double (&xv)[ZW - 1], int& lv, int64_t t0) {
         const int64_t lrow = t0 + tid < r1 ? t0 + tid : r1 - 1;
 #pragma unroll
@@ -97,7 +102,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             const int cc = c < ncols ? c : ncols - 1;
             xv[c] = a.cols[(int64_t)cc * a.col_stride + lrow];
         }
-        lv = lvbase[lrow & lvmask];
+        lv = lvbase[lrow & lvmask] & lvand;
     };
     const int col = lane & 15, sub = lane >> 4;
     auto process_tile = [&](double (&xv)[ZW - 1], int lvraw, int64_t t0) {
@@ -187,28 +192,44 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         }
         __syncthreads();
         // ---- MFMA accumulation, one bucket at a time (static register indices); the
-        // bucket bounds live in SGPRs via readlane, one operand read ahead of each MFMA
+        // bucket bounds live in SGPRs via readlane
         const int bo = lane <= NB ? boff[lane] : 0;
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            const int g0 = (__builtin_amdgcn_readlane(bo, b) >> 2) + w;
+            // wave (w + b) % 4 starts each bucket, so the odd groups spread over the waves
+            const int g0 = (__builtin_amdgcn_readlane(bo, b) >> 2) + ((w + b) & (GNW - 1));
             const int g1 = __builtin_amdgcn_readlane(bo, b + 1) >> 2;
             if (g0 >= g1) continue;
-            const double* rp = tile + (4 * g0 + sub) * RS;
-            double a0 = rp[col];
-            double a1 = NT == 2 ? rp[16 + col] : 0.0;
-            for (int g = g0; g < g1; g += GNW) {
-                const int gn = g + GNW < g1 ? g + GNW : g;
-                const double* rn = tile + (4 * gn + sub) * RS;
-                const double n0 = rn[col];
-                const double n1 = NT == 2 ? rn[16 + col] : 0.0;
-                acc0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a0, acc0[b], 0, 0, 0);
-                if (NT == 2) {
-                    acc1[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, a1, acc1[b], 0, 0, 0);
-                    acc2[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, a1, acc2[b], 0, 0, 0);
+            // 4 groups per trip: the LDS operand reads are issued together so one wait covers
+            // four MFMAs (a single read-wait-MFMA chain leaves the MFMA pipe idle)
+            const double* base = tile + sub * RS + col;
+            int g = g0;
+            for (; g + 3 * GNW < g1; g += 4 * GNW) {
+                double x0[4], x1[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double* rp = base + 4 * (g + u * GNW) * RS;
+                    x0[u] = rp[0];
+                    x1[u] = NT == 2 ? rp[16] : 0.0;
                 }
-                a0 = n0;
-                a1 = n1;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], x0[u], acc0[b], 0, 0, 0);
+                    if (NT == 2) {
+                        acc1[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], x1[u], acc1[b], 0, 0, 0);
+                        acc2[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], x1[u], acc2[b], 0, 0, 0);
+                    }
+                }
+            }
+            for (; g < g1; g += GNW) {
+                const double* rp = base + 4 * g * RS;
+                const double x0 = rp[0];
+                const double x1 = NT == 2 ? rp[16] : 0.0;
+                acc0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, x0, acc0[b], 0, 0, 0);
+                if (NT == 2) {
+                    acc1[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, x1, acc1[b], 0, 0, 0);
+                    acc2[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, x1, acc2[b], 0, 0, 0);
+                }
             }
         }
         __syncthreads();
@@ -217,6 +238,13 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     double xa[ZW - 1], xb[ZW - 1];
     int la = 0, lb = 0;
     load_tile(xa, la, r0);
+    if (tid < 128) prm[tid >> 5][tid & 31] = pv;
+    if (tid < 64) lut[tid] = (uint8_t)lutv;
+    if (tid < nmodels) {
+        mmask[tid] = (uint32_t)mmv;
+        ymask[tid] = (uint32_t)ymv;
+    }
+    __syncthreads();
     for (int64_t t0 = r0; t0 < r1;) {
         if (PF) load_tile(xb, lb, t0 + GT);
         process_tile(xa, la, t0);
@@ -243,36 +271,39 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     // ---- cross-wave reduction and store: partial[chunk][bucket][packed upper triangle]
     // (ZW*(ZW+1)/2 doubles per bucket: Z'Z is symmetric, half the bytes of a full tile)
     constexpr int PK = ZW * (ZW + 1) / 2;
+    constexpr int ZZ = ZW * ZW;
+    constexpr int NBATCH = TILE / (GNW * ZZ) < NB ? TILE / (GNW * ZZ) : NB;   // buckets per LDS pass
     const int nbr = a.npatterns * nlevels;
     double* outp = a.partial + (int64_t)chunk * nbr * PK;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        if (b >= nbr) continue;   // block-uniform
-        double* red = tile + w * ZW * ZW;
+    for (int b0 = 0; b0 < NB; b0 += NBATCH) {
+        if (b0 >= nbr) break;   // block-uniform
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = sub + 4 * r;
-            red[i * ZW + col] = acc0[b][r];
-            if (NT == 2) {
-                red[i * ZW + 16 + col] = acc1[b][r];
-                red[(16 + col) * ZW + i] = acc1[b][r];
-                red[(16 + i) * ZW + 16 + col] = acc2[b][r];
+        for (int bb = 0; bb < NBATCH; ++bb) {
+            const int b = b0 + bb;
+            if (b >= NB) continue;
+            double* red = tile + (bb * GNW + w) * ZZ;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = sub + 4 * r;
+                red[i * ZW + col] = acc0[b][r];
+                if (NT == 2) {
+                    red[i * ZW + 16 + col] = acc1[b][r];
+                    red[(16 + i) * ZW + 16 + col] = acc2[b][r];
+                }
             }
         }
         __syncthreads();
-        for (int e = tid; e < PK; e += GT) {
-            // packed index e -> (i, j), i <= j, row-major over the upper triangle
-            int i = 0, rem = e;
-            while (rem >= ZW - i) {
-                rem -= ZW - i;
-                ++i;
-            }
-            const int j = i + rem;
-            const int f = i * ZW + j;
-            double s = tile[f];
+        for (int e = tid; e < NBATCH * ZZ; e += GT) {
+            const int bb = e / ZZ, f = e - bb * ZZ;
+            const int i = f / ZW, j = f - i * ZW;
+            const int b = b0 + bb;
+            if (b < nbr && i <= j) {
+                double s = tile[bb * GNW * ZZ + f];
 #pragma unroll
-            for (int ww = 1; ww < GNW; ++ww) s += tile[ww * ZW * ZW + f];
-            outp[(int64_t)b * PK + e] = s;
+                for (int ww = 1; ww < GNW; ++ww) s += tile[(bb * GNW + ww) * ZZ + f];
+                outp[(int64_t)b * PK + i * ZW - (i * (i - 1)) / 2 + (j - i)] = s;
+            }
         }
         __syncthreads();
     }
