@@ -114,6 +114,40 @@ __device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t* scratch)
     return s;
 }
 
+template <int NW>
+__device__ __forceinline__ double block_min_f64(double v, double* scratch) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
+    const int w = threadIdx.x / WAVE;
+    __syncthreads();
+    if (lane_id() == 0) scratch[w] = v;
+    __syncthreads();
+    double s = scratch[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s = fmin(s, scratch[i]);
+    return s;
+}
+// Two sums at once (one pair of barriers); `scratch` holds 2*NW doubles.
+template <int NW>
+__device__ __forceinline__ double2 block_sum2(double a, double b, double* scratch) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    const int w = threadIdx.x / WAVE;
+    __syncthreads();
+    if (lane_id() == 0) {
+        scratch[w] = a;
+        scratch[NW + w] = b;
+    }
+    __syncthreads();
+    double2 r = make_double2(scratch[0], scratch[NW]);
+#pragma unroll
+    for (int i = 1; i < NW; ++i) {
+        r.x += scratch[i];
+        r.y += scratch[NW + i];
+    }
+    return r;
+}
+
 // Exclusive prefix sum over the block (NW waves); returns this thread's offset and the
 // block total via *total.
 template <int NW>

@@ -33,7 +33,9 @@ constexpr int GNW = GT / WAVE;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-template <int NT, int NB, int MINW, bool PF>
+// DBG (measurement builds only, FM_GRAM_DEBUG): 1 = stream the tiles and skip sort/MFMA,
+// 2 = clip + sort + scatter but no MFMA.  Results are wrong in debug modes.
+template <int NT, int NB, int MINW, bool PF, int DBG = 0>
 __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     constexpr int ZW = 16 * NT;
     constexpr int RS = ZW + 1;          // LDS row stride (doubles): conflict-free scatter
@@ -105,7 +107,14 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         lv = lvbase[lrow & lvmask] & lvand;
     };
     const int col = lane & 15, sub = lane >> 4;
+    double dbg_sink = 0.0;
     auto process_tile = [&](double (&xv)[ZW - 1], int lvraw, int64_t t0) {
+        if (DBG == 1) {
+#pragma unroll
+            for (int c = 0; c < ZW - 1; ++c) dbg_sink += xv[c];
+            dbg_sink += (double)lvraw;
+            return;
+        }
         const int64_t row = t0 + tid;
         const bool inr = row < r1;
         uint32_t nn = 0, infb = 0;
@@ -191,24 +200,30 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             }
         }
         __syncthreads();
-        // ---- MFMA accumulation, one bucket at a time (static register indices); the
-        // bucket bounds live in SGPRs via readlane
+        // ---- MFMA accumulation.  Wave w takes the contiguous quarter [W0, W1) of the sorted
+        // tile's 4-row groups, so it touches only the few buckets that overlap it (one LDS
+        // wait per bucket, not per bucket of the whole tile) and the waves stay balanced to
+        // one group.  Bucket bounds live in SGPRs via readlane; accumulators are indexed
+        // statically, so the bucket loop is unrolled and skips the buckets outside the range.
         const int bo = lane <= NB ? boff[lane] : 0;
+        const int gtot = __builtin_amdgcn_readlane(bo, NB) >> 2;
+        const int W0 = (gtot * w) / GNW, W1 = (gtot * (w + 1)) / GNW;
+        const double* base = tile + sub * RS + col;
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            // wave (w + b) % 4 starts each bucket, so the odd groups spread over the waves
-            const int g0 = (__builtin_amdgcn_readlane(bo, b) >> 2) + ((w + b) & (GNW - 1));
-            const int g1 = __builtin_amdgcn_readlane(bo, b + 1) >> 2;
+        for (int b = 0; b < (DBG == 2 ? 0 : NB); ++b) {
+            const int gb0 = __builtin_amdgcn_readlane(bo, b) >> 2;
+            const int gb1 = __builtin_amdgcn_readlane(bo, b + 1) >> 2;
+            const int g0 = gb0 > W0 ? gb0 : W0;
+            const int g1 = gb1 < W1 ? gb1 : W1;
             if (g0 >= g1) continue;
             // 4 groups per trip: the LDS operand reads are issued together so one wait covers
-            // four MFMAs (a single read-wait-MFMA chain leaves the MFMA pipe idle)
-            const double* base = tile + sub * RS + col;
+            // four MFMAs
             int g = g0;
-            for (; g + 3 * GNW < g1; g += 4 * GNW) {
+            for (; g + 3 < g1; g += 4) {
                 double x0[4], x1[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const double* rp = base + 4 * (g + u * GNW) * RS;
+                    const double* rp = base + 4 * (g + u) * RS;
                     x0[u] = rp[0];
                     x1[u] = NT == 2 ? rp[16] : 0.0;
                 }
@@ -221,7 +236,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
                     }
                 }
             }
-            for (; g < g1; g += GNW) {
+            for (; g < g1; ++g) {
                 const double* rp = base + 4 * g * RS;
                 const double x0 = rp[0];
                 const double x1 = NT == 2 ? rp[16] : 0.0;
@@ -257,6 +272,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         if (!PF && t0 < r1) load_tile(xa, la, t0);
     }
 
+    if (DBG == 1 && dbg_sink == 12345.678) a.partial[0] = dbg_sink;
     // ---- inf flags (rare): one atomic per wave per model
     const uint32_t wf = wave_or_u32(fl);
     if (lane == 0 && wf != 0) {
@@ -316,7 +332,15 @@ void launch_gram(const fm_gram_args& a, hipStream_t st) {
         const char* e = getenv("FM_GRAM_PREFETCH");
         return e ? atoi(e) : 1;
     }();
-    if (pf)
+    static const int dbg = [] {
+        const char* e = getenv("FM_GRAM_DEBUG");
+        return e ? atoi(e) : 0;
+    }();
+    if (NT == 1 && NB == 16 && dbg == 1)
+        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true, 1>), dim3(a.nchunks), dim3(GT), 0, st, a);
+    else if (NT == 1 && NB == 16 && dbg == 2)
+        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true, 2>), dim3(a.nchunks), dim3(GT), 0, st, a);
+    else if (pf)
         hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true>), dim3(a.nchunks), dim3(GT), 0, st, a);
     else
         hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false>), dim3(a.nchunks), dim3(GT), 0, st, a);

@@ -3,15 +3,15 @@
 // Replaces np.percentile(vals, 1/99) in winsorize (reference src/calc_Lewellen_2014.py:
 // 519-523) and pandas groupby(...).quantile([.2,.5]) of NYSE `me` in get_subsets (:74-82).
 //
-// One 256-thread workgroup per (segment, column).  The segment's values live in
-// registers as order-preserving uint64 keys (VPT per thread, one coalesced HBM read).
-// Ranks near either tail (the 1%/99% winsorize cuts: rank ~n/100) take a fast path:
-//   * the k-th smallest value is bounded above by tau = the k-th smallest of the 256
-//     per-thread minima (k threads each own >= 1 value <= tau), so c_le(tau) >= k+1;
-//   * at most k threads hold values < tau, so the candidates {x < tau} are few (about
-//     k); they are compacted to LDS and ranked there by counting (no sort, few barriers).
-// Middle ranks (pandas 0.2/0.5) and any overflow use an exact 8-bit LSD-free radix select
-// (MSB-first histogram narrowing) over the register keys.  Results are the exact order
+// One 256-thread workgroup per (segment, column).  The segment's values live in registers
+// as FP64 (VPT per thread, one coalesced HBM read; NaN = missing or masked out).  Both
+// winsorize tails (ranks ~n/100 from either end) are found in one pass (select_tails):
+//   * tau = the exact rj-th smallest of the 256 per-thread minima (per-wave bitonic sort
+//     + merge ranks by binary search): rj+1 threads own a value <= tau, so s[rj] <= tau;
+//   * only the values < tau can precede s[rj]; there are about rj of them, compacted
+//     to LDS with one packed scan (both tails at once) and sorted by one wave per tail.
+// Middle ranks (pandas 0.2/0.5) and any overflow use an exact MSB-first 8-bit radix
+// select over order-preserving uint64 keys formed on the fly.  Results are the exact order
 // statistics, so the interpolated cut is bit-identical to numpy/pandas given the same
 // no-FMA lerp (this file is compiled with -ffp-contract=off).
 #include <math.h>
@@ -29,7 +29,7 @@ struct SelSmem {
     uint64_t buf[CAND_CAP];
     uint32_t hist[256];
     uint64_t u64s[SNW];
-    double dbl[SNW];
+    double dbl[2 * SNW];
     int ints[8];
     uint64_t bc[4];
 };
@@ -50,17 +50,24 @@ struct SelArgs {
     double* sd;
 };
 
-// Exact key of the element at ascending rank `rank` (0-based) among non-SENT keys.
+__device__ __forceinline__ uint64_t key_of(double x) { return isnan(x) ? SENT : dkey(x); }
+
+// General path: exact key at ascending rank `rank` (0-based) among the valid values, by an
+// MSB-first 8-bit radix select over keys formed on the fly from the register values (no
+// key array, so the general path adds no registers to the tail fast path).
 template <int VPT>
-__device__ __forceinline__ uint64_t radix_rank(const uint64_t (&keys)[VPT], int rank, SelSmem& sm) {
+__device__ __forceinline__ uint64_t radix_rank(const double (&xv)[VPT], int rank, SelSmem& sm) {
     uint64_t prefix = 0, pmask = 0;
     int rem = rank;
+#pragma unroll 1
     for (int shift = 56; shift >= 0; shift -= 8) {
         for (int i = threadIdx.x; i < 256; i += ST) sm.hist[i] = 0;
         __syncthreads();
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-            const uint64_t k = keys[v];
+            double x = xv[v];
+            asm volatile("" : "+v"(x));   // keep the key per pass (no hoisted key array)
+            const uint64_t k = key_of(x);
             if (k != SENT && (k & pmask) == prefix) atomicAdd(&sm.hist[(k >> shift) & 255u], 1u);
         }
         __syncthreads();
@@ -104,100 +111,28 @@ __device__ __forceinline__ uint64_t radix_rank(const uint64_t (&keys)[VPT], int 
     return prefix;
 }
 
-// Counting rank among LDS values buf[0..M): ascending, ties broken by index (unique ranks).
-__device__ __forceinline__ int lds_rank(const uint64_t* buf, int M, uint64_t v, int self) {
-    int r = 0;
-    for (int u = 0; u < M; ++u) {
-        const uint64_t x = buf[u];
-        r += (x < v || (x == v && u < self)) ? 1 : 0;
-    }
-    return r;
-}
-
-// Keys at ascending ranks ri <= rj (< n) with the tail fast path; block-uniform.
-// tau = the rj-th smallest of the 256 per-thread minima (found by counting ranks, no sort)
-// bounds s[rj] from above; the few keys < tau are compacted to LDS and ranked by counting.
+// Keys at ranks ri <= rj (rj == ri or ri + 1) by radix select; block-uniform.
 template <int VPT>
-__device__ __forceinline__ void select_low(const uint64_t (&keys)[VPT], int ri, int rj, uint64_t& ki,
-                           uint64_t& kj, SelSmem& sm) {
-    bool done = false;
-    if (rj < ST) {
-        uint64_t m = SENT;
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) m = keys[v] < m ? keys[v] : m;
-        __syncthreads();
-        sm.buf[threadIdx.x] = m;
-        if (threadIdx.x == 0) sm.bc[0] = SENT;
-        __syncthreads();
-        if (lds_rank(sm.buf, ST, m, threadIdx.x) == rj) sm.bc[0] = m;
-        __syncthreads();
-        const uint64_t tau = sm.bc[0];
-        if (tau != SENT) {
-            int lt = 0;
-#pragma unroll
-            for (int v = 0; v < VPT; ++v) lt += keys[v] < tau ? 1 : 0;
-            int c_lt = 0;
-            const int off = block_excl_scan<SNW>(lt, sm.ints, &c_lt);
-            if (ri >= c_lt) {
-                ki = kj = tau;
-                done = true;
-            } else if (c_lt <= CAND_CAP) {
-                int o = off;
-                __syncthreads();
-#pragma unroll
-                for (int v = 0; v < VPT; ++v)
-                    if (keys[v] < tau) sm.buf[o++] = keys[v];
-                __syncthreads();
-                for (int i = threadIdx.x; i < c_lt; i += ST) {
-                    const uint64_t v = sm.buf[i];
-                    const int r = lds_rank(sm.buf, c_lt, v, i);
-                    if (r == ri) sm.bc[1] = v;
-                    if (r == rj) sm.bc[2] = v;
-                }
-                __syncthreads();
-                ki = sm.bc[1];
-                kj = rj < c_lt ? sm.bc[2] : tau;
-                __syncthreads();
-                done = true;
-            }
-        }
-    }
-    if (!done) {
-        ki = radix_rank<VPT>(keys, ri, sm);
-        if (rj == ri) {
-            kj = ki;
-        } else {
-            int le = 0;
-            uint64_t nxt = SENT;
-#pragma unroll
-            for (int v = 0; v < VPT; ++v) {
-                le += keys[v] <= ki ? 1 : 0;
-                if (keys[v] > ki && keys[v] < nxt) nxt = keys[v];
-            }
-            le = block_sum<SNW>(le, sm.ints);
-            nxt = block_min_u64<SNW>(nxt, sm.u64s);
-            kj = le >= rj + 1 ? ki : nxt;
-        }
-    }
-}
-
-// Keys at ranks ri <= rj, choosing the lower-tail, upper-tail (complemented keys) or
-// radix path.  `keys` is restored on return.
-template <int VPT>
-__device__ __forceinline__ void select_ranks(uint64_t (&keys)[VPT], int n, int ri, int rj, uint64_t& ki,
-                             uint64_t& kj, SelSmem& sm) {
-    if (rj < ST || (n - 1 - ri) >= ST) {
-        select_low<VPT>(keys, ri, rj, ki, kj, sm);
+__device__ __forceinline__ void radix_pair(const double (&xv)[VPT], int ri, int rj, uint64_t& ki,
+                                           uint64_t& kj, SelSmem& sm) {
+    ki = radix_rank<VPT>(xv, ri, sm);
+    if (rj == ri) {
+        kj = ki;
         return;
     }
+    int le = 0;
+    uint64_t nxt = SENT;
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) keys[v] = keys[v] == SENT ? SENT : ~keys[v];
-    uint64_t a, b;
-    select_low<VPT>(keys, n - 1 - rj, n - 1 - ri, a, b, sm);
-    kj = ~a;
-    ki = ~b;
-#pragma unroll
-    for (int v = 0; v < VPT; ++v) keys[v] = keys[v] == SENT ? SENT : ~keys[v];
+    for (int v = 0; v < VPT; ++v) {
+        double x = xv[v];
+        asm volatile("" : "+v"(x));
+        const uint64_t k = key_of(x);
+        le += k <= ki ? 1 : 0;
+        if (k > ki && k < nxt) nxt = k;
+    }
+    le = block_sum<SNW>(le, sm.ints);
+    nxt = block_min_u64<SNW>(nxt, sm.u64s);
+    kj = le >= rj + 1 ? ki : nxt;
 }
 
 // Bitonic sort (ascending) of the 64*R keys held by one wave: element e = lane + 64*r lives
@@ -251,81 +186,97 @@ __device__ __forceinline__ void wave_sort_lds(uint64_t* buf, int c) {
     for (int r = 0; r < R; ++r) buf[lane + WAVE * r] = v[r];
 }
 
-// Both winsorize tails at once: keys at ranks li <= lj (lower tail) and hi_i <= hi_j (upper
-// tail), n valid keys.  Returns false (nothing written, block-uniform) when the fast path
-// does not apply; the caller then uses select_ranks.
-//   tau_lo = max over the 4 waves of the wave's k-th smallest thread minimum,
-//   k = ceil((lj+1)/4): 4k >= lj+1 distinct keys are <= tau_lo, so s[lj] <= tau_lo, and
-//   only the keys < tau_lo (about lj of them) can precede it.  Same for the upper tail on
-//   complemented keys.  Candidates are compacted with one packed scan and sorted by one
-//   wave per tail.
-template <int VPT>
-__device__ __forceinline__ bool select_tails(const uint64_t (&keys)[VPT], int n, int li, int lj,
-                                             int hi_i, int hi_j, uint64_t& k0, uint64_t& k1,
-                                             uint64_t& k2, uint64_t& k3, SelSmem& sm) {
-    const int ci = n - 1 - hi_j, cj = n - 1 - hi_i;   // upper-tail ranks in complemented order
-    if (lj >= ST - 3 || cj >= ST - 3) return false;
-    uint64_t mn = SENT, cmn = SENT;
+// Number of entries of the ascending list L[0..64) that precede v in the merged order:
+// entries < v, or <= v when the list's wave comes first (ties broken by wave).
+__device__ __forceinline__ int merge_count(const uint64_t* L, uint64_t v, bool inclusive) {
+    int lo = 0;
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-        const uint64_t k = keys[v];
-        const uint64_t ck = k == SENT ? SENT : ~k;
-        mn = k < mn ? k : mn;
-        cmn = ck < cmn ? ck : cmn;
+    for (int step = 32; step > 0; step >>= 1) {
+        const uint64_t x = L[lo + step - 1];
+        lo += (x < v || (inclusive && x == v)) ? step : 0;
     }
-    uint64_t a[1] = {mn}, b[1] = {cmn};
+    const uint64_t x = L[lo < WAVE ? lo : WAVE - 1];
+    lo += (lo < WAVE && (x < v || (inclusive && x == v))) ? 1 : 0;
+    return lo;
+}
+
+// Both winsorize tails at once, on the FP64 values xv (NaN = absent): keys at ranks
+// li <= lj (lower tail) and hi_i <= hi_j (upper tail) among n valid values, thread minima
+// mn / maxima mx.  Returns false (block-uniform, nothing written) when the fast path does
+// not apply; the caller then takes the general path.
+//   tau_lo = the lj-th smallest of the 256 thread minima (exact: per-wave bitonic sort,
+//   then each lane's rank in the merged order by binary search in the other waves' lists).
+//   lj+1 threads own a value <= tau_lo, so s[lj] <= tau_lo, and only the values < tau_lo
+//   (a few more than lj) can precede it: they are compacted with one packed scan and
+//   sorted by one wave.  The upper tail is the same on complemented keys of the maxima.
+template <int VPT>
+__device__ __forceinline__ bool select_tails(const double (&xv)[VPT], double mn, double mx, int n,
+                                             int li, int lj, int hi_i, int hi_j, uint64_t& k0,
+                                             uint64_t& k1, uint64_t& k2, uint64_t& k3, SelSmem& sm) {
+    const int ci = n - 1 - hi_j, cj = n - 1 - hi_i;   // upper-tail ranks in complemented order
+    if (lj >= ST || cj >= ST) return false;
+    uint64_t a[1] = {isnan(mn) ? SENT : dkey(mn)};
+    uint64_t b[1] = {isnan(mx) ? SENT : ~dkey(mx)};
     wave_sort<1>(a);
     wave_sort<1>(b);
     const int w = threadIdx.x / WAVE, lane = lane_id();
-    const int klo = (lj + 4) / 4, khi = (cj + 4) / 4;
-    __syncthreads();   // sm.bc / sm.buf may still be read by a previous phase
-    if (lane == klo - 1) sm.buf[CAND_CAP - 8 + w] = a[0];
-    if (lane == khi - 1) sm.buf[CAND_CAP - 4 + w] = b[0];
+    uint64_t* Llo = sm.buf + CAND_CAP - 8 * WAVE;       // [4][64] sorted thread minima
+    uint64_t* Lhi = sm.buf + CAND_CAP - 4 * WAVE;       // [4][64] sorted complemented maxima
+    __syncthreads();   // sm.buf may still be read by a previous phase
+    Llo[w * WAVE + lane] = a[0];
+    Lhi[w * WAVE + lane] = b[0];
+    if (threadIdx.x < 2) sm.bc[threadIdx.x] = SENT;
     __syncthreads();
-    uint64_t tlo = 0, thi = 0;
+    // merged rank of this lane's entries (ranks >= lane, so only lanes <= lj / cj matter)
+    if (lane <= lj && a[0] != SENT) {
+        int r = lane;
 #pragma unroll
-    for (int i = 0; i < SNW; ++i) {
-        const uint64_t x = sm.buf[CAND_CAP - 8 + i], y = sm.buf[CAND_CAP - 4 + i];
-        tlo = x > tlo ? x : tlo;
-        thi = y > thi ? y : thi;
+        for (int u = 0; u < SNW; ++u)
+            if (u != w) r += merge_count(Llo + u * WAVE, a[0], u < w);
+        if (r == lj) sm.bc[0] = a[0];
     }
-    if (tlo == SENT || thi == SENT) return false;   // some wave lacks k valid thread minima
+    if (lane <= cj && b[0] != SENT) {
+        int r = lane;
+#pragma unroll
+        for (int u = 0; u < SNW; ++u)
+            if (u != w) r += merge_count(Lhi + u * WAVE, b[0], u < w);
+        if (r == cj) sm.bc[1] = b[0];
+    }
+    __syncthreads();
+    const uint64_t tlo_k = sm.bc[0], thi_k = sm.bc[1];
+    if (tlo_k == SENT || thi_k == SENT) return false;   // fewer valid thread minima than needed
+    const double tlo = kval(tlo_k), thi = kval(~thi_k);
     int cnt = 0;
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-        const uint64_t k = keys[v];
-        const uint64_t ck = k == SENT ? SENT : ~k;
-        cnt += (k < tlo ? 1 : 0) + (ck < thi ? 0x10000 : 0);
-    }
+    for (int v = 0; v < VPT; ++v) cnt += (xv[v] < tlo ? 1 : 0) + (xv[v] > thi ? 0x10000 : 0);
     int tot = 0;
     const int off = block_excl_scan<SNW>(cnt, sm.ints, &tot);
     const int clo = tot & 0xFFFF, chi = tot >> 16;
-    constexpr int HALF = CAND_CAP / 2;
-    if (clo > 2 * WAVE || chi > 2 * WAVE) return false;   // block-uniform
+    constexpr int HALF = CAND_CAP / 4;
+    if (clo > 4 * WAVE || chi > 4 * WAVE) return false;   // block-uniform
     {
         int ol = off & 0xFFFF, oh = HALF + (off >> 16);
-        __syncthreads();
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-            const uint64_t k = keys[v];
-            const uint64_t ck = k == SENT ? SENT : ~k;
-            if (k < tlo) sm.buf[ol++] = k;
-            if (ck < thi) sm.buf[oh++] = ck;
+            if (xv[v] < tlo) sm.buf[ol++] = dkey(xv[v]);
+            if (xv[v] > thi) sm.buf[oh++] = ~dkey(xv[v]);
         }
         __syncthreads();
     }
     if (w == 0) {
         if (clo <= WAVE) wave_sort_lds<1>(sm.buf, clo);
-        else wave_sort_lds<2>(sm.buf, clo);
+        else if (clo <= 2 * WAVE) wave_sort_lds<2>(sm.buf, clo);
+        else wave_sort_lds<4>(sm.buf, clo);
     } else if (w == 1) {
         if (chi <= WAVE) wave_sort_lds<1>(sm.buf + HALF, chi);
-        else wave_sort_lds<2>(sm.buf + HALF, chi);
+        else if (chi <= 2 * WAVE) wave_sort_lds<2>(sm.buf + HALF, chi);
+        else wave_sort_lds<4>(sm.buf + HALF, chi);
     }
     __syncthreads();
-    k0 = li < clo ? sm.buf[li] : tlo;
-    k1 = lj < clo ? sm.buf[lj] : tlo;
-    const uint64_t ca = ci < chi ? sm.buf[HALF + ci] : thi;
-    const uint64_t cb = cj < chi ? sm.buf[HALF + cj] : thi;
+    k0 = li < clo ? sm.buf[li] : tlo_k;
+    k1 = lj < clo ? sm.buf[lj] : tlo_k;
+    const uint64_t ca = ci < chi ? sm.buf[HALF + ci] : thi_k;
+    const uint64_t cb = cj < chi ? sm.buf[HALF + cj] : thi_k;
     k3 = ~ca;   // rank hi_j (complemented rank ci)
     k2 = ~cb;   // rank hi_i
     return true;
@@ -368,32 +319,28 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
     const int64_t r0 = a.seg_off[s];
     const int L = (int)(a.seg_off[s + 1] - r0);
     const double* src = a.cols + (int64_t)c * a.col_stride + r0;
-    uint64_t keys[VPT];
-    int cnt = 0;
     // Unconditional loads (index clamped, masked after): a load under a runtime condition
     // makes hipcc wait vmcnt(0) per load and serializes the HBM round trips.
     const int last = L > 0 ? L - 1 : 0;
+    const uint8_t* mbase = a.mask ? a.mask + r0 : (const uint8_t*)src;
+    const int mand = a.mask ? 0xFF : 0, mor = a.mask ? 0 : 1;
     double xv[VPT];
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
         const int idx = threadIdx.x + v * ST;
-        xv[v] = L > 0 ? src[idx < L ? idx : last] : NAN;
+        const int ci = idx < L ? idx : last;
+        const double x = src[ci];
+        const int m = (mbase[ci] & mand) | mor;
+        xv[v] = (idx < L && m != 0) ? x : NAN;
     }
-    uint8_t mk[VPT];
-    if (a.mask != nullptr) {
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-            const int idx = threadIdx.x + v * ST;
-            mk[v] = L > 0 ? a.mask[r0 + (idx < L ? idx : last)] : 0;
-        }
-    }
+    // thread count / min / max (fmin/fmax ignore NaN)
+    int cnt = 0;
+    double mn = NAN, mx = NAN;
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
-        const int idx = threadIdx.x + v * ST;
-        const bool on = idx < L && (a.mask == nullptr || mk[v] != 0) && !isnan(xv[v]);
-        const uint64_t k = on ? dkey(xv[v]) : SENT;
-        keys[v] = k;
-        cnt += on ? 1 : 0;
+        cnt += isnan(xv[v]) ? 0 : 1;
+        mn = fmin(mn, xv[v]);
+        mx = fmax(mx, xv[v]);
     }
     const int n = block_sum<SNW>(cnt, sm.ints);
     double lo = NAN, hi = NAN;
@@ -404,44 +351,43 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
         qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
         uint64_t k0, k1, k2, k3;
-        if (!select_tails<VPT>(keys, n, i0, j0, i1, j1, k0, k1, k2, k3, sm)) {
-            select_ranks<VPT>(keys, n, i0, j0, k0, k1, sm);
-            select_ranks<VPT>(keys, n, i1, j1, k2, k3, sm);
+        if (!select_tails<VPT>(xv, mn, mx, n, i0, j0, i1, j1, k0, k1, k2, k3, sm)) {
+            radix_pair<VPT>(xv, i0, j0, k0, k1, sm);
+            radix_pair<VPT>(xv, i1, j1, k2, k3, sm);
         }
         lo = qlerp(kval(k0), kval(k1), g0, a.lerp_mode);
         hi = qlerp(kval(k2), kval(k3), g1, a.lerp_mode);
     }
     if (a.mean != nullptr) {
-        // moments of the clipped values (pandas clip ignores NaN bounds)
-        double sum = 0.0;
+        // Moments of the clipped values (pandas clip ignores NaN bounds).  One pass about a
+        // pivot p inside the data (a finite cut, else the smallest finite value):
+        // mean = p + S1/n, var = (S2 - S1^2/n)/(n-1).
+        double p = isfinite(lo) ? lo : (isfinite(hi) ? hi : 0.0);
+        if (!isfinite(lo) && !isfinite(hi)) {
+            // no cuts (short month): pivot = the smallest finite value
+            double m2 = isfinite(mn) ? mn : NAN;
+            p = block_min_f64<SNW>(m2, sm.dbl);
+            if (!isfinite(p)) p = 0.0;
+        }
+        double s1 = 0.0, s2 = 0.0;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-            if (keys[v] == SENT) continue;
-            double x = kval(keys[v]);
-            if (apply) {
-                if (x < lo) x = lo;
-                if (x > hi) x = hi;
-            }
-            sum += x;
+            double x = xv[v];
+            if (x < lo) x = lo;
+            if (x > hi) x = hi;
+            const double d = isnan(x) ? 0.0 : x - p;
+            s1 += d;
+            s2 = fma(d, d, s2);
         }
-        sum = block_sum<SNW>(sum, sm.dbl);
-        const double mu = n > 0 ? sum / (double)n : NAN;
-        double ss = 0.0;
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-            if (keys[v] == SENT) continue;
-            double x = kval(keys[v]);
-            if (apply) {
-                if (x < lo) x = lo;
-                if (x > hi) x = hi;
-            }
-            const double d = x - mu;
-            ss += d * d;
-        }
-        ss = block_sum<SNW>(ss, sm.dbl);
+        double2 r = block_sum2<SNW>(s1, s2, sm.dbl);
         if (threadIdx.x == 0) {
+            const double mu = n > 0 ? p + r.x / (double)n : NAN;
             a.mean[(int64_t)c * a.nseg + s] = mu;
-            if (a.sd) a.sd[(int64_t)c * a.nseg + s] = n > 1 ? sqrt(ss / (double)(n - 1)) : NAN;
+            if (a.sd) {
+                double var = n > 1 ? (r.y - r.x * (r.x / (double)n)) / (double)(n - 1) : NAN;
+                if (var < 0.0) var = 0.0;
+                a.sd[(int64_t)c * a.nseg + s] = n > 1 ? sqrt(var) : NAN;
+            }
         }
     }
     if (threadIdx.x == 0) {
@@ -481,6 +427,7 @@ extern "C" int fm_select_cuts(const double* cols, int64_t col_stride, int32_t nc
     else if (vpt <= 4) launch_select<4>(a, ncols, st);
     else if (vpt <= 8) launch_select<8>(a, ncols, st);
     else if (vpt <= 16) launch_select<16>(a, ncols, st);
+    else if (vpt <= 20) launch_select<20>(a, ncols, st);
     else if (vpt <= 24) launch_select<24>(a, ncols, st);
     else if (vpt <= 32) launch_select<32>(a, ncols, st);
     else if (vpt <= 48) launch_select<48>(a, ncols, st);
