@@ -5,21 +5,25 @@
 // subsetting of get_subsets (src/calc_Lewellen_2014.py:95-105) and the X'X / X'y / y'y
 // formation inside sm.OLS (src/regressions.py:57, src/calc_Lewellen_2014.py:917-919).
 //
-// Data flow per workgroup (one chunk of one month; 256 threads = 4 waves):
-//   1. each thread streams one row of the chunk tile: ncols coalesced FP64 loads (one per
-//      column, SoA), clip to the month's winsorize cuts, NaN/inf tests, shift by the
-//      month's pivot (optional standardize scale), z = [1, x..., y] with NaN -> 0;
+// One workgroup (256 threads = 4 waves) per chunk of one month.  The waves work
+// independently (no workgroup barrier inside the row loop): wave w takes the 64-row tiles
+// w, w+4, w+8, ... of the chunk, and per tile
+//   1. each lane streams one row: ncols coalesced FP64 loads (SoA; the next tile's loads are
+//      in flight while this one is processed), clip to the month's winsorize cuts, NaN/inf
+//      tests, shift by the month's pivot (optional standardize scale), z = [1, x..., y] with
+//      NaN -> 0;
 //   2. the row's validity pattern (bit m: every column model m needs is non-NaN) and its
-//      universe level give a bucket id; a wave-ballot counting sort scatters the tile
-//      into LDS grouped by bucket, each bucket padded to a multiple of 4 rows;
-//   3. each wave walks 4-row groups of the sorted tile and issues
-//      v_mfma_f64_16x16x4_f64 with A = B = the group's z rows (lane l holds
-//      z[row l>>4][col l&15]), accumulating Z^T Z per bucket in registers (16x16 FP64
-//      tile = 4 doubles per lane; two tiles wide for up to 31 columns).
+//      universe level give a bucket id; per bucket one wave ballot gives the bucket's row
+//      count (SGPR) and the lane's rank, so the counting sort needs no LDS counters; each
+//      lane writes its z row to the wave's private LDS tile at (bucket offset + rank);
+//   3. per bucket, v_mfma_f64_16x16x4_f64 with A = B = 4 rows of that bucket (lane l holds
+//      z[row l>>4][col l&15]; rows past the bucket's count read as 0) accumulates Z^T Z in
+//      registers (16x16 FP64 tile = 4 doubles per lane; two tiles wide for > 15 columns).
 // At chunk end the four waves' accumulators are summed through LDS and written as one
-// packed upper-triangular Gram per (chunk, bucket).  fm_solve combines buckets into problems: model m's
-// Gram is the sum over patterns that contain m and levels >= the problem's universe,
-// restricted to m's columns.  One HBM read of the panel serves every model x universe.
+// packed upper-triangular Gram per (chunk, bucket).  fm_solve combines buckets into
+// problems: model m's Gram is the sum over patterns that contain m and levels >= the
+// problem's universe, restricted to m's columns.  One HBM read of the panel serves every
+// model x universe.
 #include <math.h>
 #include <stdlib.h>
 
@@ -33,22 +37,71 @@ constexpr int GNW = GT / WAVE;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// DBG (measurement builds only, FM_GRAM_DEBUG): 1 = stream the tiles and skip sort/MFMA,
-// 2 = clip + sort + scatter but no MFMA.  Results are wrong in debug modes.
-template <int NT, int NB, int MINW, bool PF, int DBG = 0>
+// Hardware v_max_f64 / v_min_f64 (IEEE mode: a quiet-NaN operand yields the other one).
+// Inline asm, because the maxnum/minnum lowering canonicalizes both inputs first (two extra
+// v_max_f64 per call).
+__device__ __forceinline__ double hw_max(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double hw_min(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// nn = 2 * nn + (x is not NaN): one compare + one add-with-carry
+__device__ __forceinline__ uint32_t push_valid(uint32_t nn, double x) {
+    asm("v_cmp_o_f64 vcc, %1, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(nn) : "v"(x) : "vcc");
+    return nn;
+}
+
+// 4x4 block pairs (I, J) of the ZW x ZW Gram covered by the 4x4x4 MFMAs of one 4-row group.
+// v_mfma_f64_4x4x4_4b: lane l = x + 4*blk + 16*k holds A[blk][x][k] and B[blk][k][x], and
+// D[blk][i][j] lands at lane j + 4*blk + 16*i.
+//  * NT == 1 (16 columns): "rotation" cover.  Instruction k pairs block row blk with block
+//    column (blk + k) % 4, k = 0..2: the diagonal blocks, the 4 blocks one step off (one of
+//    them transposed) and the 2 blocks two steps off (computed twice).  Every lane's A
+//    operand is z[row][q] (q = lane & 15) for all three instructions and its B operands are
+//    z[row][q + 4k] with the row's columns 0..7 repeated at 16..23 in LDS, so one address
+//    VGPR serves all three reads (immediate offsets).
+//  * NT == 2 (32 columns): the 36 upper pairs in row order, 4 per instruction (9), A / B
+//    column offsets per lane from the table.
+template <int NBLK>
+struct BlockPairs {
+    static constexpr int P = NBLK * (NBLK + 1) / 2;
+    static constexpr int NI = (P + 3) / 4;
+    int I[NI * 4], J[NI * 4];
+    constexpr BlockPairs() : I(), J() {
+        int p = 0;
+        for (int i = 0; i < NBLK; ++i)
+            for (int j = i; j < NBLK; ++j) {
+                I[p] = i;
+                J[p] = j;
+                ++p;
+            }
+        for (; p < NI * 4; ++p) I[p] = J[p] = 0;
+    }
+};
+
+// One workgroup per chunk (normally a whole month: the chunk plan makes chunks as large as
+// the chip's resident workgroup slots allow, so the prologue and the cross-wave epilogue run
+// once per month and every wave streams ~20 tiles back to back).  MINW = waves per SIMD.
+template <int NT, int NB, int MINW>
 __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     constexpr int ZW = 16 * NT;
-    constexpr int RS = ZW + 1;          // LDS row stride (doubles): conflict-free scatter
-    constexpr int ROWS = GT + 3 * NB;   // sorted tile incl. padding rows
-    constexpr int TILE = ROWS * RS > GNW * ZW * ZW ? ROWS * RS : GNW * ZW * ZW;
-    __shared__ double tile[TILE];
+    constexpr int RS = ZW + 1;              // LDS row stride (doubles): conflict-free scatter
+    constexpr int TR = WAVE;                // rows per wave tile (one per lane)
+    constexpr int WT = TR * RS;             // one wave's sorted tile
+    constexpr int PK = ZW * (ZW + 1) / 2;   // packed upper triangle
+    constexpr BlockPairs<4 * NT> BP{};
+    constexpr int NI = NT == 1 ? 3 : BlockPairs<8>::NI;   // 4x4x4 MFMAs per 4-row group
+    constexpr int NBATCH = (GNW * WT) / (GNW * PK) < NB ? (GNW * WT) / (GNW * PK) : NB;
+    static_assert(NBATCH >= 1, "epilogue image does not fit the tile area");
+    __shared__ double tile[GNW * WT];
+    __shared__ double zblk[4 * RS];         // four zero rows: operands of padded group slots
     __shared__ double prm[4][32];
-    __shared__ int wcnt[GNW][NB];
-    __shared__ int woff[GNW][NB];
-    __shared__ int boff[NB + 1];
-    __shared__ int btot[NB];
     __shared__ uint8_t lut[64];
-    __shared__ uint32_t mmask[FM_MAX_MODELS], ymask[FM_MAX_MODELS];
 
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
@@ -57,11 +110,14 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     const int seg = a.chunk_seg[chunk];
     const int64_t r0 = a.chunk_row[2 * chunk], r1 = a.chunk_row[2 * chunk + 1];
     const int ncols = a.ncols, nseg = a.nseg, nmodels = a.nmodels, nlevels = a.nlevels;
+    const int ntile = (int)((r1 - r0 + TR - 1) / TR);
+    const bool scaled = a.inv_scale != nullptr;
 
-    // Prologue loads are unconditional (pointer/index selected, value masked after) and are
-    // issued before the first tile, so they cost one HBM round trip, not one per load.
+    // Prologue loads (month parameters, pattern table, model masks) are unconditional
+    // (pointer/index selected, value masked after) and issued before the first tile's row
+    // loads, so waiting for them does not wait for the tile.
     double pv;
-    int lutv, mmv, ymv;
+    int lutv, mmv;
     {
         const int kind = tid >> 5, c = tid & 31;
         const double* src = kind == 0 ? a.lo : kind == 1 ? a.hi : kind == 2 ? a.shift : a.inv_scale;
@@ -72,225 +128,186 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         pv = on ? v : dflt;
         const int npat = 1 << nmodels;
         lutv = a.pattern_id[tid < npat ? tid : 0];
-        const int mi = tid < nmodels ? tid : 0;
+        const int mi = lane < nmodels ? lane : 0;   // read back per wave by readlane
         mmv = (int)a.model_mask[mi];
-        ymv = (int)a.model_ymask[mi];
     }
-    d4 acc0[NB], acc1[NB], acc2[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        acc0[b] = d4{0.0, 0.0, 0.0, 0.0};
-        if (NT == 2) {
-            acc1[b] = d4{0.0, 0.0, 0.0, 0.0};
-            acc2[b] = d4{0.0, 0.0, 0.0, 0.0};
-        }
-    }
-    uint32_t fl = 0;   // bit 2m: inf in a regressor of model m; bit 2m+1: inf in its y
 
-    // Software pipeline, two register buffers: tile t+1's loads are issued before tile t
-    // is sorted and accumulated (no copy between buffers, which would force vmcnt(0)).
-    // Loads are unconditional (row and column clamped in range, results masked after): a
-    // load under a runtime condition makes hipcc wait vmcnt(0) per load.
-    // Without universes the level load reads byte 0 of the panel and is masked to 0.  The base
-    // must be a kernel-argument pointer: a __device__ global would make it a flat load, which
-    // also counts in lgkmcnt, so every LDS wait of the tile would wait for HBM.
+    // Row loads: one wave-uniform base per column (s_add in the scalar unit) + the lane's
+    // 32-bit row offset, so every load is a global_load with an SGPR base and no per-load
+    // address VALU.  Lanes past the chunk end re-read its last row (masked later).  Without
+    // universes the level load reads byte 0 of the panel and is masked to 0.
     const uint8_t* lvbase = a.level ? a.level : (const uint8_t*)a.cols;
-    const int64_t lvmask = a.level ? ~(int64_t)0 : 0;   // address select, not a conditional load
     const int lvand = a.level ? 0xFF : 0;
-    auto load_tile = [&](double (&xv)[ZW - 1], int& lv, int64_t t0) {
-        const int64_t lrow = t0 + tid < r1 ? t0 + tid : r1 - 1;
+    const uint32_t colmask = ncols >= 32 ? ~0u : (1u << ncols) - 1u;
+    typedef const __attribute__((address_space(1))) char* gptr;   // global_load, not flat_load
+    auto load_row = [&](double (&xv)[ZW - 1], int& lv, int t) {
+        const int64_t t0 = r0 + (int64_t)t * TR;
+        const int64_t last = r1 - 1 - t0;
+        const uint32_t lo = last < 0 ? 0u : (last < lane ? (uint32_t)last : (uint32_t)lane);
+        const int64_t tb = last < 0 ? r1 - 1 : t0;   // wave-uniform tile base (clamped)
+        const double* cb = a.cols + tb;               // column 0; s_add per column
 #pragma unroll
         for (int c = 0; c < ZW - 1; ++c) {
-            const int cc = c < ncols ? c : ncols - 1;
-            xv[c] = a.cols[(int64_t)cc * a.col_stride + lrow];
+            xv[c] = *(const __attribute__((address_space(1))) double*)((gptr)cb + lo * 8u);
+            cb += c + 1 < ncols ? a.col_stride : 0;   // columns past ncols re-read the last
+            // opaque to the optimizer: otherwise it turns a repeated address into a register
+            // copy of the previous load behind a branch, i.e. a vmcnt(0) wait per column
+            asm("" : "+s"(cb));
         }
-        lv = lvbase[lrow & lvmask] & lvand;
+        // raw byte; masked where it is used (masking here would wait for the load)
+        lv = *((gptr)(a.level ? lvbase + tb : lvbase) + (a.level ? lo : 0u));
     };
-    const int col = lane & 15, sub = lane >> 4;
-    double dbg_sink = 0.0;
-    auto process_tile = [&](double (&xv)[ZW - 1], int lvraw, int64_t t0) {
-        if (DBG == 1) {
-#pragma unroll
-            for (int c = 0; c < ZW - 1; ++c) dbg_sink += xv[c];
-            dbg_sink += (double)lvraw;
-            return;
-        }
-        const int64_t row = t0 + tid;
-        const bool inr = row < r1;
-        uint32_t nn = 0, infb = 0;
-#pragma unroll
-        for (int c = 0; c < ZW - 1; ++c) {
-            double x = xv[c];
-            const double l = prm[0][c], h = prm[1][c];
-            if (x < l) x = l;   // pandas clip semantics: NaN stays, NaN bound ignored
-            if (x > h) x = h;
-            const bool ok = c < ncols && inr && !isnan(x);
-            nn |= ok ? 1u << c : 0u;
-            infb |= (ok && isinf(x)) ? 1u << c : 0u;
-            xv[c] = x;
-        }
-        uint32_t pat = 0;
-        for (int m = 0; m < nmodels; ++m)
-            if ((nn & mmask[m]) == mmask[m]) pat |= 1u << m;
-        const int pid = inr ? (int)lut[pat] : 255;
-        int bucket = -1;
-        if (pid != 255) {
-            const int lvl = lvraw < nlevels ? lvraw : nlevels - 1;
-            bucket = pid * nlevels + lvl;
-        }
-        if (infb != 0 && bucket >= 0) {
-            for (int m = 0; m < nmodels; ++m) {
-                if (!((pat >> m) & 1u)) continue;
-                if (infb & mmask[m] & ~ymask[m]) fl |= 1u << (2 * m);
-                if (infb & ymask[m]) fl |= 1u << (2 * m + 1);
-            }
-        }
-        // ---- counting sort of the tile by bucket (wave ballots; deterministic order)
-        int rank = 0;
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const uint64_t mb = __ballot(bucket == b);
-            if (bucket == b) rank = mask_rank(mb);
-            if (lane == 0) wcnt[w][b] = __popcll(mb);
-        }
-        __syncthreads();
-        if (w == 0) {
-            // bucket offsets, each bucket padded to a multiple of 4 rows (lane b = bucket b)
-            int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-            if (lane < NB) {
-                c0 = wcnt[0][lane];
-                c1 = wcnt[1][lane];
-                c2 = wcnt[2][lane];
-                c3 = wcnt[3][lane];
-            }
-            const int tot = c0 + c1 + c2 + c3;
-            const int pad = (tot + 3) & ~3;
-            int x = pad;
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-                const int y = __shfl_up(x, o, WAVE);
-                if (lane >= o) x += y;
-            }
-            const int off = x - pad;
-            if (lane < NB) {
-                boff[lane] = off;
-                btot[lane] = tot;
-                woff[0][lane] = off;
-                woff[1][lane] = off + c0;
-                woff[2][lane] = off + c0 + c1;
-                woff[3][lane] = off + c0 + c1 + c2;
-            }
-            if (lane == NB - 1) boff[NB] = off + pad;
-        }
-        __syncthreads();
-        if (bucket >= 0) {
-            // z = [1, (x - shift) * inv_scale ..., 0 pad], NaN -> 0
-            double* dst = tile + (woff[w][bucket] + rank) * RS;
-            dst[0] = 1.0;
-#pragma unroll
-            for (int c = 0; c < ZW - 1; ++c)
-                dst[1 + c] = ((nn >> c) & 1u) ? (xv[c] - prm[2][c]) * prm[3][c] : 0.0;
-        }
-        if (tid < NB * 3) {
-            const int b = tid / 3, k = tid - 3 * (tid / 3);
-            const int rp = boff[b] + btot[b] + k;
-            if (rp < boff[b + 1]) {
-#pragma unroll
-                for (int c = 0; c < ZW; ++c) tile[rp * RS + c] = 0.0;
-            }
-        }
-        __syncthreads();
-        // ---- MFMA accumulation.  Wave w takes the contiguous quarter [W0, W1) of the sorted
-        // tile's 4-row groups, so it touches only the few buckets that overlap it (one LDS
-        // wait per bucket, not per bucket of the whole tile) and the waves stay balanced to
-        // one group.  Bucket bounds live in SGPRs via readlane; accumulators are indexed
-        // statically, so the bucket loop is unrolled and skips the buckets outside the range.
-        const int bo = lane <= NB ? boff[lane] : 0;
-        const int gtot = __builtin_amdgcn_readlane(bo, NB) >> 2;
-        const int W0 = (gtot * w) / GNW, W1 = (gtot * (w + 1)) / GNW;
-        const double* base = tile + sub * RS + col;
-#pragma unroll
-        for (int b = 0; b < (DBG == 2 ? 0 : NB); ++b) {
-            const int gb0 = __builtin_amdgcn_readlane(bo, b) >> 2;
-            const int gb1 = __builtin_amdgcn_readlane(bo, b + 1) >> 2;
-            const int g0 = gb0 > W0 ? gb0 : W0;
-            const int g1 = gb1 < W1 ? gb1 : W1;
-            if (g0 >= g1) continue;
-            // 4 groups per trip: the LDS operand reads are issued together so one wait covers
-            // four MFMAs
-            int g = g0;
-            for (; g + 3 < g1; g += 4) {
-                double x0[4], x1[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const double* rp = base + 4 * (g + u) * RS;
-                    x0[u] = rp[0];
-                    x1[u] = NT == 2 ? rp[16] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    acc0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], x0[u], acc0[b], 0, 0, 0);
-                    if (NT == 2) {
-                        acc1[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[u], x1[u], acc1[b], 0, 0, 0);
-                        acc2[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[u], x1[u], acc2[b], 0, 0, 0);
-                    }
-                }
-            }
-            for (; g < g1; ++g) {
-                const double* rp = base + 4 * g * RS;
-                const double x0 = rp[0];
-                const double x1 = NT == 2 ? rp[16] : 0.0;
-                acc0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, x0, acc0[b], 0, 0, 0);
-                if (NT == 2) {
-                    acc1[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, x1, acc1[b], 0, 0, 0);
-                    acc2[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, x1, acc2[b], 0, 0, 0);
-                }
-            }
-        }
-        __syncthreads();
-    };
+    double xv[ZW - 1];   // ONE register buffer: the next tile's loads are issued as soon as
+    int lv = 0;          // this tile's values sit in LDS, and fly during its MFMAs
+    if (w < ntile) load_row(xv, lv, w);
 
-    double xa[ZW - 1], xb[ZW - 1];
-    int la = 0, lb = 0;
-    load_tile(xa, la, r0);
+    double acc[NB][NI];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int k = 0; k < NI; ++k) acc[b][k] = 0.0;
+    double* wt = tile + w * WT;   // this wave's sorted tile
+    // MFMA operand offsets (lane l = x + 4*blk + 16*kr holds row kr of the 4-row group):
+    //  NT 1: A = z[kr][q] (q = l & 15) for all three instructions, B = z[kr][(q + 4k) & 15]
+    //  NT 2: A / B columns of block pair 4k + blk from the table
+    const int kx = lane & 3, kb = (lane >> 2) & 3, kr = lane >> 4;
+    int oa[NI], ob[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        oa[k] = kr * RS + (NT == 1 ? lane & 15 : 4 * BP.I[4 * k + kb] + kx);
+        ob[k] = kr * RS + (NT == 1 ? ((lane & 15) + 4 * k) & 15 : 4 * BP.J[4 * k + kb] + kx);
+    }
+    for (int e = tid; e < 4 * RS; e += GT) zblk[e] = 0.0;
     if (tid < 128) prm[tid >> 5][tid & 31] = pv;
     if (tid < 64) lut[tid] = (uint8_t)lutv;
-    if (tid < nmodels) {
-        mmask[tid] = (uint32_t)mmv;
-        ymask[tid] = (uint32_t)ymv;
-    }
     __syncthreads();
-    for (int64_t t0 = r0; t0 < r1;) {
-        if (PF) load_tile(xb, lb, t0 + GT);
-        process_tile(xa, la, t0);
-        t0 += GT;
-        if (t0 >= r1) break;
-        if (!PF) load_tile(xb, lb, t0);
-        if (PF) load_tile(xa, la, t0 + GT);
-        process_tile(xb, lb, t0);
-        t0 += GT;
-        if (!PF && t0 < r1) load_tile(xa, la, t0);
-    }
+    // model column masks in SGPRs (wave-uniform; statically indexed below)
+    uint32_t mm[FM_MAX_MODELS];
+#pragma unroll
+    for (int m = 0; m < FM_MAX_MODELS; ++m)
+        mm[m] = (uint32_t)__builtin_amdgcn_readlane(mmv, m < nmodels ? m : 0);
 
-    if (DBG == 1 && dbg_sink == 12345.678) a.partial[0] = dbg_sink;
-    // ---- inf flags (rare): one atomic per wave per model
-    const uint32_t wf = wave_or_u32(fl);
-    if (lane == 0 && wf != 0) {
-        for (int m = 0; m < nmodels; ++m) {
-            uint32_t bits = 0;
-            if ((wf >> (2 * m)) & 1u) bits |= FM_ST_INF_IN_X;
-            if ((wf >> (2 * m + 1)) & 1u) bits |= FM_ST_INF_IN_Y;
-            if (bits) atomicOr(&a.flags[(int64_t)seg * nmodels + m], bits);
+    for (int t = w; t < ntile; t += GNW) {
+        const int64_t row = r0 + (int64_t)t * TR + lane;
+        // validity bits of the raw values (NaN = missing; clipping never makes or removes
+        // a NaN: pandas clip ignores NaN bounds)
+        uint32_t nn = 0;
+#pragma unroll
+        for (int c = ZW - 2; c >= 0; --c) nn = push_valid(nn, xv[c]);
+        const bool inr = row < r1;
+        nn &= inr ? colmask : 0u;
+        uint32_t pat = 0;
+#pragma unroll
+        for (int m = 0; m < FM_MAX_MODELS; ++m)
+            if (m < nmodels && (nn & mm[m]) == mm[m]) pat |= 1u << m;
+        const int pid = inr ? (int)lut[pat] : 255;
+        const int lvm = lv & lvand;
+        const int lvl = lvm < nlevels ? lvm : nlevels - 1;
+        const int bucket = pid != 255 ? pid * nlevels + lvl : -1;
+        // ---- wave counting sort by bucket, from KB bit ballots: this lane's slot is the
+        // number of valid lanes with a smaller bucket plus its rank among equal buckets
+        // (bitwise magnitude compare, MSB first); per-bucket counts are scalar.
+        constexpr int KB = NB <= 1 ? 0 : NB <= 2 ? 1 : NB <= 4 ? 2 : NB <= 8 ? 3 : 4;
+        const bool valid = bucket >= 0;
+        const uint64_t bv = __ballot(valid);
+        uint64_t bit[KB > 0 ? KB : 1];
+#pragma unroll
+        for (int i = 0; i < KB; ++i) bit[i] = __ballot(valid && ((bucket >> i) & 1));
+        uint32_t eql = (uint32_t)bv, eqh = (uint32_t)(bv >> 32), ltl = 0, lth = 0;
+#pragma unroll
+        for (int i = KB - 1; i >= 0; --i) {
+            const uint32_t tm = 0u - (uint32_t)((bucket >> i) & 1);
+            const uint32_t bl = (uint32_t)bit[i], bh = (uint32_t)(bit[i] >> 32);
+            ltl |= eql & ~bl & tm;
+            lth |= eqh & ~bh & tm;
+            eql &= ~(bl ^ tm);
+            eqh &= ~(bh ^ tm);
         }
+        const int dest = __popc(ltl) + __popc(lth) +
+                         (int)__builtin_amdgcn_mbcnt_hi(eqh, __builtin_amdgcn_mbcnt_lo(eql, 0u));
+        // z = [1, (clip(x) - shift) * inv_scale ...].  Missing values are NOT zeroed: a
+        // column that is NaN in a row belongs to no model of the row's pattern, so the
+        // Gram entries it pollutes are never read by fm_solve.  clip = hardware max/min: a
+        // NaN bound is ignored, a NaN x gives a don't-care value.  Dropped rows are not
+        // stored.
+        if (valid) {
+            double* dst = wt + dest * RS;
+            dst[0] = 1.0;
+            if (scaled) {
+#pragma unroll
+                for (int c = 0; c < ZW - 1; ++c)
+                    dst[1 + c] = (hw_min(hw_max(xv[c], prm[0][c]), prm[1][c]) - prm[2][c]) * prm[3][c];
+            } else {
+#pragma unroll
+                for (int c = 0; c < ZW - 1; ++c)
+                    dst[1 + c] = hw_min(hw_max(xv[c], prm[0][c]), prm[1][c]) - prm[2][c];
+            }
+        }
+        // this tile's values are consumed: the next tile's loads fly during the MFMAs
+        if (t + GNW < ntile) load_row(xv, lv, t + GNW);
+        // the operand reads below read other lanes' rows of this wave: LDS executes one
+        // wave's DS instructions in order, so only compiler reordering must be prevented
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- MFMA accumulation per bucket: NI independent 4x4x4 block products per 4-row
+        // group; in the bucket's last (partial) group the lanes of rows past the count read
+        // the zero rows instead.
+        // per-bucket counts are popcounts of the ballot masks, formed on the fly (scalar)
+        const double* rp = wt;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            uint64_t mb = bv;
+#pragma unroll
+            for (int i = 0; i < KB; ++i) mb &= ((b >> i) & 1) ? bit[i] : ~bit[i];
+            const int n = (int)__popcll(mb);
+            int g = 0;
+            for (; g + 4 <= n; g += 4, rp += 4 * RS) {
+#pragma unroll
+                for (int k = 0; k < NI; ++k)
+                    acc[b][k] = __builtin_amdgcn_mfma_f64_4x4x4f64(rp[oa[k]], rp[ob[k]], acc[b][k], 0, 0, 0);
+            }
+            if (g < n) {
+                const double* bp = g + kr < n ? rp : zblk;
+#pragma unroll
+                for (int k = 0; k < NI; ++k)
+                    acc[b][k] = __builtin_amdgcn_mfma_f64_4x4x4f64(bp[oa[k]], bp[ob[k]], acc[b][k], 0, 0, 0);
+                rp += (n - g) * RS;
+            }
+        }
+        // the next tile's scatter overwrites this tile: every operand read above has been
+        // consumed by its MFMA (data dependence), and the fences keep the order
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 
-    // ---- cross-wave reduction and store: partial[chunk][bucket][packed upper triangle]
-    // (ZW*(ZW+1)/2 doubles per bucket: Z'Z is symmetric, half the bytes of a full tile)
-    constexpr int PK = ZW * (ZW + 1) / 2;
-    constexpr int ZZ = ZW * ZW;
-    constexpr int NBATCH = TILE / (GNW * ZZ) < NB ? TILE / (GNW * ZZ) : NB;   // buckets per LDS pass
+    // ---- cross-wave reduction and store: partial[chunk][bucket][packed upper triangle].
+    // v_mfma_f64_4x4x4f64 leaves D[blk][i][j] in lane j + 4*blk + 16*i; each lane maps its
+    // entry of instruction k to the packed index of (min(r, c), max(r, c)), or -1 where the
+    // entry is a duplicate (NT 1: the two-step blocks computed twice; diagonal blocks: the
+    // strictly lower half), so every packed entry is written exactly once per wave.
     const int nbr = a.npatterns * nlevels;
     double* outp = a.partial + (int64_t)chunk * nbr * PK;
+    int od[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        int r, c;
+        bool keep;
+        if (NT == 1) {
+            r = 4 * kb + kr;
+            c = 4 * ((kb + k) & 3) + kx;
+            keep = !(k == 2 && kb >= 2) && !(k == 0 && kr > kx);
+        } else {
+            const int p = 4 * k + kb;
+            r = 4 * BP.I[p] + kr;
+            c = 4 * BP.J[p] + kx;
+            keep = p < BlockPairs<8>::P && !(BP.I[p] == BP.J[p] && kr > kx);
+        }
+        const int i = r < c ? r : c, j = r < c ? c : r;
+        od[k] = keep ? i * ZW - (i * (i - 1)) / 2 + (j - i) : -1;
+    }
+    __syncthreads();   // every wave is done with its sorted tile
 #pragma unroll
     for (int b0 = 0; b0 < NB; b0 += NBATCH) {
         if (b0 >= nbr) break;   // block-uniform
@@ -298,27 +315,20 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         for (int bb = 0; bb < NBATCH; ++bb) {
             const int b = b0 + bb;
             if (b >= NB) continue;
-            double* red = tile + (bb * GNW + w) * ZZ;
+            double* img = tile + (w * NBATCH + bb) * PK;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = sub + 4 * r;
-                red[i * ZW + col] = acc0[b][r];
-                if (NT == 2) {
-                    red[i * ZW + 16 + col] = acc1[b][r];
-                    red[(16 + i) * ZW + 16 + col] = acc2[b][r];
-                }
-            }
+            for (int k = 0; k < NI; ++k)
+                if (od[k] >= 0) img[od[k]] = acc[b][k];
         }
         __syncthreads();
-        for (int e = tid; e < NBATCH * ZZ; e += GT) {
-            const int bb = e / ZZ, f = e - bb * ZZ;
-            const int i = f / ZW, j = f - i * ZW;
+        for (int e = tid; e < NBATCH * PK; e += GT) {
+            const int bb = e / PK, f = e - bb * PK;
             const int b = b0 + bb;
-            if (b < nbr && i <= j) {
-                double s = tile[bb * GNW * ZZ + f];
+            if (b < nbr) {
+                double s = tile[bb * PK + f];
 #pragma unroll
-                for (int ww = 1; ww < GNW; ++ww) s += tile[(bb * GNW + ww) * ZZ + f];
-                outp[(int64_t)b * PK + i * ZW - (i * (i - 1)) / 2 + (j - i)] = s;
+                for (int ww = 1; ww < GNW; ++ww) s += tile[(ww * NBATCH + bb) * PK + f];
+                outp[(int64_t)b * PK + f] = s;
             }
         }
         __syncthreads();
@@ -327,23 +337,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 
 template <int NT, int NB, int MINW>
 void launch_gram(const fm_gram_args& a, hipStream_t st) {
-    // FM_GRAM_PREFETCH=0 selects the non-pipelined variant (A/B measurements)
-    static const int pf = [] {
-        const char* e = getenv("FM_GRAM_PREFETCH");
-        return e ? atoi(e) : 1;
-    }();
-    static const int dbg = [] {
-        const char* e = getenv("FM_GRAM_DEBUG");
-        return e ? atoi(e) : 0;
-    }();
-    if (NT == 1 && NB == 16 && dbg == 1)
-        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true, 1>), dim3(a.nchunks), dim3(GT), 0, st, a);
-    else if (NT == 1 && NB == 16 && dbg == 2)
-        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true, 2>), dim3(a.nchunks), dim3(GT), 0, st, a);
-    else if (pf)
-        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true>), dim3(a.nchunks), dim3(GT), 0, st, a);
-    else
-        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false>), dim3(a.nchunks), dim3(GT), 0, st, a);
+    hipLaunchKernelGGL((gram_kernel<NT, NB, MINW>), dim3(a.nchunks), dim3(GT), 0, st, a);
 }
 
 }  // namespace
@@ -366,18 +360,20 @@ extern "C" int fm_gram(const fm_gram_args* args, void* stream) {
     const int nb = a.npatterns * a.nlevels;
     hipStream_t st = (hipStream_t)stream;
     if (a.ncols <= 15) {
-        if (nb <= 1) launch_gram<1, 1, 2>(a, st);
-        else if (nb <= 4) launch_gram<1, 4, 2>(a, st);
-        else if (nb <= 8) launch_gram<1, 8, 2>(a, st);
-        else if (nb <= 16) launch_gram<1, 16, 2>(a, st);
+        if (nb <= 1) launch_gram<1, 1, 3>(a, st);
+        else if (nb <= 4) launch_gram<1, 4, 3>(a, st);
+        else if (nb <= 8) launch_gram<1, 8, 3>(a, st);
+        else if (nb <= 12) launch_gram<1, 12, 3>(a, st);
+        else if (nb <= 15) launch_gram<1, 15, 3>(a, st);   // 5 patterns x 3 universes (Table 2)
+        else if (nb <= 16) launch_gram<1, 16, 3>(a, st);
         else {
             set_error("fm_gram: %d buckets exceed 16 for <=15 columns", nb);
             return FM_ETOOBIG;
         }
     } else {
-        if (nb <= 1) launch_gram<2, 1, 1>(a, st);
-        else if (nb <= 4) launch_gram<2, 4, 1>(a, st);
-        else if (nb <= 8) launch_gram<2, 8, 1>(a, st);
+        if (nb <= 1) launch_gram<2, 1, 2>(a, st);
+        else if (nb <= 4) launch_gram<2, 4, 2>(a, st);
+        else if (nb <= 8) launch_gram<2, 8, 2>(a, st);
         else {
             set_error("fm_gram: %d buckets exceed 8 for >15 columns", nb);
             return FM_ETOOBIG;

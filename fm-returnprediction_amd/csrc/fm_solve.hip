@@ -131,6 +131,20 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
         const double n = ws.A[0];
         const int64_t ro = ((int64_t)s * a.nprob + p) * rs;
         uint32_t st = 0;
+        // inf in the problem's rows (statsmodels MissingDataError / pinv(X)@y = +-inf): a
+        // regressor or y value of +-inf makes its Gram diagonal entry sum(z^2) = +inf (the
+        // z of a finite value stays finite; entries of columns the problem does not use,
+        // which may hold NaN / inf garbage, are never read here)
+        {
+            bool infx = false, infy = false;
+            if (lane >= 1 && lane < nz) {
+                const bool d = isinf(ws.A[lane * MD + lane]);
+                infx = d && lane <= K;
+                infy = d && lane == K + 1;
+            }
+            if (__ballot(infx) != 0) st |= FM_ST_INF_IN_X;
+            if (__ballot(infy) != 0) st |= FM_ST_INF_IN_Y;
+        }
         if (a.gram_flags) st |= a.gram_flags[(int64_t)s * a.nmodels + m] & (FM_ST_INF_IN_X | FM_ST_INF_IN_Y);
         if (!(n >= (double)(K + 1))) {
             for (int k = lane; k < rs; k += WAVE) a.rec[ro + k] = k == a.pmax + 1 ? n : NAN;

@@ -321,10 +321,12 @@ def group_models(models: Sequence[Model], nlevels, cap):
     return groups
 
 
-def default_chunk_rows(total_rows, nseg, max_seg_len, target_chunks=2048):
-    """Rows per Gram workgroup: whole months when there are enough months to fill the chip,
-    else months split into ~target_chunks/nseg pieces.  Callers that shard months across
-    ranks pass the GLOBAL sizes so every rank chunks (and sums) identically."""
+def default_chunk_rows(total_rows, nseg, max_seg_len, target_chunks=512):
+    """Rows per Gram workgroup: whole months when there are enough months to fill the chip
+    (fm_gram keeps 3 workgroups per CU resident, 768 slots: one month per workgroup means one
+    prologue and one cross-wave epilogue per month), else months split into
+    ~target_chunks/nseg pieces.  Callers that shard months across ranks pass the GLOBAL sizes
+    so every rank chunks (and sums) identically."""
     if nseg == 0:
         return 256
     per = max(1, -(-target_chunks // nseg))

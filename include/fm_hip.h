@@ -90,7 +90,8 @@ typedef struct fm_gram_args {
     const uint8_t* pattern_id;    /* [1<<nmodels] validity pattern -> id, 255 = drop row */
     int32_t npatterns;            /* buckets = npatterns * nlevels */
     double* partial;              /* [nchunks][nbuckets][zw*(zw+1)/2] packed upper triangle, zw = 16 or 32 */
-    uint32_t* flags;              /* [nseg][nmodels], OR-ed FM_ST_INF_IN_X / _Y; zeroed by caller */
+    uint32_t* flags;              /* [nseg][nmodels] reserved (not written: fm_solve detects inf in
+                                     X / y per problem from the Gram diagonal); zeroed by caller */
 } fm_gram_args;
 
 typedef struct fm_solve_args {
@@ -108,7 +109,7 @@ typedef struct fm_solve_args {
     const int32_t* prob_nz;       /* [nprob] number of z indices P+1 (<= 32) */
     const int32_t* prob_flags;    /* [nprob] bit0: check nonzero-constant columns */
     const double* add_back;       /* [ncols][nseg] shift to add back for raw intercept, or NULL */
-    const uint32_t* gram_flags;   /* [nseg][nmodels] from fm_gram, or NULL */
+    const uint32_t* gram_flags;   /* [nseg][nmodels] extra FM_ST_INF_* bits OR-ed in, or NULL */
     int32_t nmodels;
     int32_t pmax;                 /* >= max P (= K+1) over problems, <= 32 */
     double* rec;                  /* [nseg][nprob][pmax+2]: intercept, slopes..., NaN pad,
