@@ -41,6 +41,27 @@ __device__ __forceinline__ double kval(uint64_t k) {
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
+// 64-bit readlane (the builtin takes 32-bit operands: a 64-bit argument is truncated)
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Hardware v_max_f64 / v_min_f64 (IEEE mode: a quiet-NaN operand yields the other one).
+// Inline asm, because the maxnum/minnum lowering canonicalizes its inputs first: an extra
+// v_max_f64 per operand, and a second register copy of every value kept for later use.
+__device__ __forceinline__ double hw_max(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double hw_min(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // number of set bits of `mask` strictly below this lane
 __device__ __forceinline__ int mask_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),

@@ -37,19 +37,6 @@ constexpr int GNW = GT / WAVE;
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// Hardware v_max_f64 / v_min_f64 (IEEE mode: a quiet-NaN operand yields the other one).
-// Inline asm, because the maxnum/minnum lowering canonicalizes both inputs first (two extra
-// v_max_f64 per call).
-__device__ __forceinline__ double hw_max(double a, double b) {
-    double r;
-    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ double hw_min(double a, double b) {
-    double r;
-    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
 // nn = 2 * nn + (x is not NaN): one compare + one add-with-carry
 __device__ __forceinline__ uint32_t push_valid(uint32_t nn, double x) {
     asm("v_cmp_o_f64 vcc, %1, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(nn) : "v"(x) : "vcc");

@@ -39,6 +39,7 @@ struct SelArgs {
     int64_t col_stride;
     const int64_t* seg_off;
     int nseg;
+    int ncols;
     const uint8_t* mask;
     double q_lo, q_hi;
     int min_count;
@@ -48,6 +49,7 @@ struct SelArgs {
     int32_t* nvalid;
     double* mean;
     double* sd;
+    double* center;
 };
 
 __device__ __forceinline__ uint64_t key_of(double x) { return isnan(x) ? SENT : dkey(x); }
@@ -167,6 +169,57 @@ __device__ __forceinline__ void wave_sort(uint64_t (&v)[R]) {
                     v[r] = take_min ? mn : mx;
                 }
             }
+        }
+    }
+}
+
+// Non-NaN doubles (element e = lane + 64 r in register r): bitonic sort ascending with the
+// hardware min / max (no 64-bit integer compares and selects).
+template <int R>
+__device__ __forceinline__ void wave_sort_f64(double (&v)[R]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= WAVE * R; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= WAVE) {
+                const int rj = j / WAVE;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (r & rj) continue;
+                    const bool up = (((lane + WAVE * r) & k) == 0);
+                    const double mn = hw_min(v[r], v[r | rj]), mx = hw_max(v[r], v[r | rj]);
+                    v[r] = up ? mn : mx;
+                    v[r | rj] = up ? mx : mn;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const double p = __shfl_xor(v[r], j, WAVE);
+                    const bool up = (((lane + WAVE * r) & k) == 0);
+                    const bool lower = (lane & j) == 0;
+                    v[r] = lower == up ? hw_min(p, v[r]) : hw_max(p, v[r]);
+                }
+            }
+        }
+    }
+}
+
+// 32-bit keys, R == 1: one wave sorts its 64 lane values ascending (21 stages, one
+// ds_bpermute each, min/max instead of 64-bit compares and selects).
+template <int R>
+__device__ __forceinline__ void wave_sort32(uint32_t (&v)[R]) {
+    static_assert(R == 1, "wave_sort32: one register");
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= WAVE; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t p = (uint32_t)__shfl_xor((int)v[0], j, WAVE);
+            const bool up = (lane & k) == 0;
+            const bool lower = (lane & j) == 0;
+            const uint32_t mn = p < v[0] ? p : v[0], mx = p < v[0] ? v[0] : p;
+            v[0] = lower == up ? mn : mx;
         }
     }
 }
@@ -311,11 +364,10 @@ __device__ __forceinline__ double qlerp(double a, double b, double g, int mode) 
     return g == 0.0 ? a : a + (b - a) * g;
 }
 
+// One (segment, column) unit on a 256-thread workgroup: the general path (any ranks, row
+// masks, up to 96 * 256 rows).  Block-uniform control flow.
 template <int VPT>
-__global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
-    __shared__ SelSmem sm;
-    const int s = blockIdx.x;
-    const int c = blockIdx.y;
+__device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, SelSmem& sm) {
     const int64_t r0 = a.seg_off[s];
     const int L = (int)(a.seg_off[s + 1] - r0);
     const double* src = a.cols + (int64_t)c * a.col_stride + r0;
@@ -333,14 +385,14 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         const int m = (mbase[ci] & mand) | mor;
         xv[v] = (idx < L && m != 0) ? x : NAN;
     }
-    // thread count / min / max (fmin/fmax ignore NaN)
+    // thread count / min / max (NaN-ignoring hardware min / max)
     int cnt = 0;
     double mn = NAN, mx = NAN;
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
         cnt += isnan(xv[v]) ? 0 : 1;
-        mn = fmin(mn, xv[v]);
-        mx = fmax(mx, xv[v]);
+        mn = hw_min(mn, xv[v]);
+        mx = hw_max(mx, xv[v]);
     }
     const int n = block_sum<SNW>(cnt, sm.ints);
     double lo = NAN, hi = NAN;
@@ -357,6 +409,18 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         }
         lo = qlerp(kval(k0), kval(k1), g0, a.lerp_mode);
         hi = qlerp(kval(k2), kval(k3), g1, a.lerp_mode);
+    }
+    if (a.center != nullptr) {
+        // Gram pivot: the midpoint of the cuts, else of the values' range, else 0 (block-
+        // uniform branch: lo / hi are block-uniform)
+        double cen = 0.5 * (lo + hi);
+        if (!isfinite(cen)) {
+            const double m1 = block_min_f64<SNW>(isfinite(mn) ? mn : NAN, sm.dbl);
+            const double m2 = -block_min_f64<SNW>(isfinite(mx) ? -mx : NAN, sm.dbl);
+            cen = 0.5 * (m1 + m2);
+            if (!isfinite(cen)) cen = 0.0;
+        }
+        if (threadIdx.x == 0) a.center[(int64_t)c * a.nseg + s] = cen;
     }
     if (a.mean != nullptr) {
         // Moments of the clipped values (pandas clip ignores NaN bounds).  One pass about a
@@ -398,10 +462,227 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
     }
 }
 
+// fallback == 0: one unit per workgroup (grid nseg x ncols).  fallback == 1: a fixed grid
+// that walks every unit and redoes those the wave kernel marked with nvalid == -1.
+template <int VPT, bool FB>
+__global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
+    __shared__ SelSmem sm;
+    if (!FB) {
+        select_unit_wg<VPT>(a, blockIdx.x, blockIdx.y, sm);
+        return;
+    }
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
+    for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+        if (__builtin_amdgcn_readfirstlane(a.nvalid[u]) != -1) continue;   // block-uniform
+        __syncthreads();   // sm is reused across units
+        select_unit_wg<VPT>(a, (int)(u % a.nseg), (int)(u / a.nseg), sm);
+    }
+}
+
 template <int VPT>
-void launch_select(const SelArgs& a, int ncols, hipStream_t st) {
-    dim3 grid(a.nseg, ncols);
-    hipLaunchKernelGGL(select_kernel<VPT>, grid, dim3(ST), 0, st, a);
+void launch_select(const SelArgs& a, int ncols, hipStream_t st, bool fallback) {
+    if (fallback)
+        hipLaunchKernelGGL((select_kernel<VPT, true>), dim3(1024), dim3(ST), 0, st, a);
+    else
+        hipLaunchKernelGGL((select_kernel<VPT, false>), dim3(a.nseg, ncols), dim3(ST), 0, st, a);
+}
+
+// ---------------------------------------------------------------------------------------
+// Wave-per-unit fast path for the winsorize tails (no row mask): one wave holds a whole
+// (segment, column) in registers (VPL values per lane, element lane + 64 v), so there is
+// no workgroup barrier at all and twice as many units per CU are in flight as with the
+// workgroup kernel.  Per unit:
+//   * n, lane minima / maxima; tau_lo = the lj-th smallest lane minimum (one 64-key wave
+//     bitonic sort): lj+1 lanes own a value <= tau_lo, so s[lj] <= tau_lo, and only the
+//     values < tau_lo can precede it.  Same for the upper tail on complemented keys.
+//   * those candidates (about 1.8% of n at n = 5000) are compacted by ballot + mbcnt into
+//     the wave's LDS list and sorted by a 128-key wave bitonic sort; the order statistics
+//     are read at wave-uniform positions.
+// Units the fast path cannot finish (ranks >= 64, more than 128 candidates, fewer lanes
+// with a valid value than the rank) get nvalid = -1 and are redone by the workgroup
+// kernel's fallback pass.  Results are exact order statistics either way.
+constexpr int WCAP = 128;
+
+template <int VPL>
+__global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
+    __shared__ double cbuf[SNW][2][WCAP];   // per wave: lower / upper tail candidates
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+    const int64_t u = (int64_t)blockIdx.x * SNW + w;
+    if (u >= (int64_t)a.nseg * a.ncols) return;   // wave-uniform; no block barriers below
+    const int s = (int)(u % a.nseg), c = (int)(u / a.nseg);
+    const int64_t r0 = a.seg_off[s];
+    const int L = (int)(a.seg_off[s + 1] - r0);
+    typedef const __attribute__((address_space(1))) char* gptr;   // global_load, SGPR base
+    const gptr src = (gptr)(a.cols + (int64_t)c * a.col_stride + r0);
+    const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
+    // All loads are issued before any value is used (clamped 32-bit byte offsets, no
+    // masking here: masking at the load would make each load wait for its data).
+    double xv[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+        const uint32_t off = (uint32_t)(lane + v * WAVE) * 8u;
+        xv[v] = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    int cnt = 0;
+    double mn = NAN, mx = NAN;
+    const int vfull = L / WAVE;   // rows v < vfull lie inside the segment (wave-uniform)
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+        if (v >= vfull && lane + v * WAVE >= L) xv[v] = NAN;   // past the segment end
+        cnt += isnan(xv[v]) ? 0 : 1;
+        mn = hw_min(mn, xv[v]);   // NaN-ignoring, no canonicalized copy of xv
+        mx = hw_max(mx, xv[v]);
+    }
+    const int n = __builtin_amdgcn_readfirstlane(wave_sum(cnt));
+    double lo = NAN, hi = NAN;
+    if (n >= a.min_count && n > 0) {
+        int i0, j0, i1, j1;
+        double g0, g1;
+        qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
+        qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
+        const int ci = n - 1 - j1, cj = n - 1 - i1;   // upper ranks in complemented order
+        bool ok = j0 < WAVE && cj < WAVE;
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+        if (ok) {
+            // tau from the high 32 bits of the keys (half the cost of a 64-bit sort): the
+            // j0-th smallest high word T bounds j0+1 lane minima by key (T << 32 | ~0), so
+            // that key is as valid a tau as an exact lane minimum (and s[j0] is a candidate
+            // whenever tau is not itself a data value)
+            uint32_t ta[1] = {isnan(mn) ? 0xFFFFFFFFu : (uint32_t)(dkey(mn) >> 32)};
+            uint32_t tb[1] = {isnan(mx) ? 0xFFFFFFFFu : (uint32_t)(~dkey(mx) >> 32)};
+            wave_sort32<1>(ta);
+            wave_sort32<1>(tb);
+            const uint32_t Ta = (uint32_t)__builtin_amdgcn_readlane((int)ta[0], j0);
+            const uint32_t Tb = (uint32_t)__builtin_amdgcn_readlane((int)tb[0], cj);
+            ok = Ta != 0xFFFFFFFFu && Tb != 0xFFFFFFFFu;
+            if (ok) {
+                double tlo = kval(((uint64_t)Ta << 32) | 0xFFFFFFFFull);
+                double thi = kval(~(((uint64_t)Tb << 32) | 0xFFFFFFFFull));
+                if (isnan(tlo)) tlo = INFINITY;    // high word of +inf's key
+                if (isnan(thi)) thi = -INFINITY;   // high word of -inf's complemented key
+                double* Ll = cbuf[w][0];
+                double* Lh = cbuf[w][1];
+                int clo = 0, chi = 0;   // wave-uniform running counts; overflow is checked once
+#pragma unroll
+                for (int v = 0; v < VPL; ++v) {
+                    const bool bl = xv[v] < tlo, bh = xv[v] > thi;
+                    const uint64_t ml = __ballot(bl), mh = __ballot(bh);
+                    if (ml) {
+                        if (bl) Ll[(clo + mask_rank(ml)) & (WCAP - 1)] = xv[v];
+                        clo += (int)__popcll(ml);
+                    }
+                    if (mh) {
+                        if (bh) Lh[(chi + mask_rank(mh)) & (WCAP - 1)] = -xv[v];   // ascending
+                        chi += (int)__popcll(mh);
+                    }
+                }
+                ok = clo <= WCAP && chi <= WCAP;
+                if (ok) {
+                    // LDS executes one wave's DS instructions in order; only the compiler's
+                    // reordering must be fenced
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // the candidates are never NaN: sort them as doubles (hardware min/max;
+                    // equal values, +0 / -0 included, are interchangeable for the result)
+                    double la[2], lb[2];
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const int e = lane + WAVE * r;
+                        la[r] = e < clo ? Ll[e] : INFINITY;
+                        lb[r] = e < chi ? Lh[e] : INFINITY;
+                    }
+                    wave_sort_f64<2>(la);
+                    wave_sort_f64<2>(lb);
+                    auto at = [&](const double (&v)[2], int e) -> double {
+                        const uint64_t b = readlane_u64((uint64_t)__double_as_longlong((e >> 6) ? v[1] : v[0]),
+                                                        e & 63);
+                        return __longlong_as_double((long long)b);
+                    };
+                    v0 = i0 < clo ? at(la, i0) : tlo;
+                    v1 = j0 < clo ? at(la, j0) : tlo;
+                    v3 = ci < chi ? -at(lb, ci) : thi;   // rank j1
+                    v2 = cj < chi ? -at(lb, cj) : thi;   // rank i1
+                }
+            }
+        }
+        if (!ok) {
+            if (lane == 0 && a.nvalid) a.nvalid[u] = -1;   // redone by the fallback pass
+            return;
+        }
+        lo = qlerp(v0, v1, g0, a.lerp_mode);
+        hi = qlerp(v2, v3, g1, a.lerp_mode);
+    }
+    if (a.center != nullptr) {
+        // Gram pivot: the midpoint of the cuts, else of the values' range, else 0
+        double cen = 0.5 * (lo + hi);
+        if (!isfinite(cen)) {
+            double m1 = isfinite(mn) ? mn : NAN, m2 = isfinite(mx) ? mx : NAN;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                m1 = hw_min(m1, __shfl_xor(m1, o, WAVE));
+                m2 = hw_max(m2, __shfl_xor(m2, o, WAVE));
+            }
+            cen = 0.5 * (m1 + m2);
+            if (!isfinite(cen)) cen = 0.0;
+        }
+        if (lane == 0) a.center[u] = cen;
+    }
+    if (a.mean != nullptr) {
+        // moments of the clipped values about a pivot inside the data (see select_unit_wg)
+        double p = isfinite(lo) ? lo : (isfinite(hi) ? hi : 0.0);
+        if (!isfinite(lo) && !isfinite(hi)) {
+            double m2 = isfinite(mn) ? mn : NAN;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m2 = fmin(m2, __shfl_xor(m2, o, WAVE));
+            p = isfinite(m2) ? m2 : 0.0;
+        }
+        double s1 = 0.0, s2 = 0.0;
+        if (isfinite(lo) && !isnan(hi)) {
+            // p == lo: hardware max/min send a NaN (absent) value to lo, so it adds d == 0
+            // exactly; the same d as the general loop for every present value
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                const double d = hw_min(hw_max(xv[v], lo), hi) - lo;
+                s1 += d;
+                s2 = fma(d, d, s2);
+            }
+        } else {
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                double x = xv[v];
+                if (x < lo) x = lo;
+                if (x > hi) x = hi;
+                const double d = isnan(x) ? 0.0 : x - p;
+                s1 += d;
+                s2 = fma(d, d, s2);
+            }
+        }
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if (lane == 0) {
+            a.mean[u] = n > 0 ? p + s1 / (double)n : NAN;
+            if (a.sd) {
+                double var = n > 1 ? (s2 - s1 * (s1 / (double)n)) / (double)(n - 1) : NAN;
+                if (var < 0.0) var = 0.0;
+                a.sd[u] = n > 1 ? sqrt(var) : NAN;
+            }
+        }
+    }
+    if (lane == 0) {
+        a.lo[u] = lo;
+        a.hi[u] = hi;
+        if (a.nvalid) a.nvalid[u] = n;
+    }
+}
+
+template <int VPL>
+void launch_select_wave(const SelArgs& a, hipStream_t st) {
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
+    hipLaunchKernelGGL(select_wave_kernel<VPL>, dim3((unsigned)((nunits + SNW - 1) / SNW)), dim3(ST), 0,
+                       st, a);
 }
 
 }  // namespace
@@ -412,32 +693,59 @@ extern "C" int fm_select_cuts(const double* cols, int64_t col_stride, int32_t nc
                               const uint8_t* row_mask, double q_lo, double q_hi,
                               int32_t min_count, int32_t lerp_mode, double* lo, double* hi,
                               int32_t* nvalid, double* mean, double* sd, void* stream) {
+    const fm_select_args a{cols,    col_stride, ncols,    seg_off, nseg, max_seg_len, row_mask, q_lo,
+                           q_hi,    min_count,  lerp_mode, lo,     hi,   nvalid,      mean,     sd,
+                           nullptr};
+    return fm_select(&a, stream);
+}
+
+extern "C" int fm_select(const fm_select_args* args, void* stream) {
     using namespace fm;
-    FM_REQUIRE(cols && seg_off && lo && hi, "fm_select_cuts: null pointer");
+    FM_REQUIRE(args != nullptr, "fm_select: null args");
+    const fm_select_args& x = *args;
+    const double* cols = x.cols;
+    const int64_t* seg_off = x.seg_off;
+    const int32_t ncols = x.ncols, nseg = x.nseg, max_seg_len = x.max_seg_len;
+    const uint8_t* row_mask = x.row_mask;
+    const int32_t* nvalid = x.nvalid;
+    FM_REQUIRE(cols && seg_off && x.lo && x.hi, "fm_select_cuts: null pointer");
     FM_REQUIRE(ncols > 0 && ncols <= 65535 && nseg >= 0, "fm_select_cuts: bad sizes");
-    FM_REQUIRE(lerp_mode == 0 || lerp_mode == 1, "fm_select_cuts: lerp_mode must be 0 or 1");
-    FM_REQUIRE(q_lo >= 0.0 && q_lo <= 1.0 && q_hi >= 0.0 && q_hi <= 1.0,
+    FM_REQUIRE(x.lerp_mode == 0 || x.lerp_mode == 1, "fm_select_cuts: lerp_mode must be 0 or 1");
+    FM_REQUIRE(x.q_lo >= 0.0 && x.q_lo <= 1.0 && x.q_hi >= 0.0 && x.q_hi <= 1.0,
                "fm_select_cuts: quantiles must be in [0,1]");
     if (nseg == 0) return FM_OK;
-    SelArgs a{cols, col_stride, seg_off, nseg, row_mask, q_lo, q_hi, min_count, lerp_mode,
-              lo, hi, nvalid, mean, sd};
+    SelArgs a{cols,        x.col_stride, seg_off, nseg,     ncols, row_mask, x.q_lo, x.q_hi,
+              x.min_count, x.lerp_mode,  x.lo,    x.hi,     x.nvalid, x.mean, x.sd,  x.center};
     hipStream_t st = (hipStream_t)stream;
     const int vpt = (max_seg_len + ST - 1) / ST;
-    if (vpt <= 2) launch_select<2>(a, ncols, st);
-    else if (vpt <= 4) launch_select<4>(a, ncols, st);
-    else if (vpt <= 8) launch_select<8>(a, ncols, st);
-    else if (vpt <= 16) launch_select<16>(a, ncols, st);
-    else if (vpt <= 20) launch_select<20>(a, ncols, st);
-    else if (vpt <= 24) launch_select<24>(a, ncols, st);
-    else if (vpt <= 32) launch_select<32>(a, ncols, st);
-    else if (vpt <= 48) launch_select<48>(a, ncols, st);
-    else if (vpt <= 64) launch_select<64>(a, ncols, st);
-    else if (vpt <= 96) launch_select<96>(a, ncols, st);
-    else {
+    if (vpt > 96) {
         set_error("fm_select_cuts: segment of %d rows exceeds the %d-row register budget",
                   max_seg_len, 96 * ST);
         return FM_ETOOBIG;
     }
+    // wave fast path: no row mask, segments of <= 96 * 64 rows, nvalid present (it carries
+    // the fallback marks); the workgroup kernel then redoes the marked units only
+    const int vpl = (max_seg_len + WAVE - 1) / WAVE;
+    const bool wave = row_mask == nullptr && nvalid != nullptr && vpl <= 96;
+    if (wave) {
+        if (vpl <= 16) launch_select_wave<16>(a, st);
+        else if (vpl <= 32) launch_select_wave<32>(a, st);
+        else if (vpl <= 48) launch_select_wave<48>(a, st);
+        else if (vpl <= 64) launch_select_wave<64>(a, st);
+        else if (vpl <= 80) launch_select_wave<80>(a, st);
+        else launch_select_wave<96>(a, st);
+        FM_CHECK_LAUNCH("fm_select_cuts(wave)");
+    }
+    if (vpt <= 2) launch_select<2>(a, ncols, st, wave);
+    else if (vpt <= 4) launch_select<4>(a, ncols, st, wave);
+    else if (vpt <= 8) launch_select<8>(a, ncols, st, wave);
+    else if (vpt <= 16) launch_select<16>(a, ncols, st, wave);
+    else if (vpt <= 20) launch_select<20>(a, ncols, st, wave);
+    else if (vpt <= 24) launch_select<24>(a, ncols, st, wave);
+    else if (vpt <= 32) launch_select<32>(a, ncols, st, wave);
+    else if (vpt <= 48) launch_select<48>(a, ncols, st, wave);
+    else if (vpt <= 64) launch_select<64>(a, ncols, st, wave);
+    else launch_select<96>(a, ncols, st, wave);
     FM_CHECK_LAUNCH("fm_select_cuts");
     return FM_OK;
 }

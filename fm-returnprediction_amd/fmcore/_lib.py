@@ -43,6 +43,15 @@ class GramArgs(C.Structure):
     ]
 
 
+class SelectArgs(C.Structure):
+    _fields_ = [
+        ("cols", _p), ("col_stride", _i64), ("ncols", _i32), ("seg_off", _p), ("nseg", _i32),
+        ("max_seg_len", _i32), ("row_mask", _p), ("q_lo", _f64), ("q_hi", _f64),
+        ("min_count", _i32), ("lerp_mode", _i32), ("lo", _p), ("hi", _p), ("nvalid", _p),
+        ("mean", _p), ("sd", _p), ("center", _p),
+    ]
+
+
 class SolveArgs(C.Structure):
     _fields_ = [
         ("partial", _p), ("seg_chunk_off", _p), ("nseg", _i32), ("zw", _i32),
@@ -62,6 +71,7 @@ _SIGS = {
     "fm_abi_sizes": (_i32, [C.POINTER(_i32), C.POINTER(_i32)]),
     "fm_select_cuts": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _f64, _f64, _i32, _i32,
                               _p, _p, _p, _p, _p, _p]),
+    "fm_select": (_i32, [C.POINTER(SelectArgs), _p]),
     "fm_clip": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_standardize": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_universe_level": (_i32, [_p, _p, _i32, _i64, _p, _p, _p, _p]),

@@ -182,11 +182,13 @@ class Cuts:
     nvalid: torch.Tensor  # [C, T] int32
     mean: Optional[torch.Tensor] = None
     sd: Optional[torch.Tensor] = None
+    center: Optional[torch.Tensor] = None   # Gram pivot (midpoint of the cuts)
 
 
 def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols=None,
-                row_mask=None, moments=False, tag="fm_select_cuts"):
-    """Per (column, month) quantile cuts.  ``cols`` defaults to panel.cols."""
+                row_mask=None, moments=False, center=False, tag="fm_select_cuts"):
+    """Per (column, month) quantile cuts.  ``cols`` defaults to panel.cols.  ``moments``:
+    also the clipped mean / sd; ``center``: also a Gram pivot inside the data (fm_select)."""
     src = panel.cols if cols is None else cols
     if src.dim() == 1:
         src = src.view(1, -1)
@@ -195,14 +197,18 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
     lo = torch.empty((C, T), dtype=torch.float64, device=dev)
     hi = torch.empty_like(lo)
     nv = torch.empty((C, T), dtype=torch.int32, device=dev)
-    mean = sd = None
+    mean = sd = cen = None
     if moments:
         mean = torch.empty_like(lo)
         sd = torch.empty_like(lo)
-    _kcall(tag, "fm_select_cuts", src.data_ptr(), src.stride(0), C, panel.seg_off.data_ptr(), T,
-           max(panel.max_seg_len, 1), _ptr(row_mask), float(q_lo), float(q_hi), int(min_count),
-           int(mode), lo.data_ptr(), hi.data_ptr(), nv.data_ptr(), _ptr(mean), _ptr(sd), _stream())
-    return Cuts(lo, hi, nv, mean, sd)
+    if center:
+        cen = torch.empty_like(lo)
+    sa = L.SelectArgs(cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, seg_off=panel.seg_off.data_ptr(),
+                      nseg=T, max_seg_len=max(panel.max_seg_len, 1), row_mask=_ptr(row_mask), q_lo=float(q_lo),
+                      q_hi=float(q_hi), min_count=int(min_count), lerp_mode=int(mode), lo=lo.data_ptr(),
+                      hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=_ptr(mean), sd=_ptr(sd), center=_ptr(cen))
+    _kcall(tag, "fm_select", L.C.byref(sa), _stream())
+    return Cuts(lo, hi, nv, mean, sd, cen)
 
 
 def clip(panel: DevicePanel, cuts: Cuts, out=None):

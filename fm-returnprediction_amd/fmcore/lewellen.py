@@ -112,12 +112,15 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
     inv_scale = None
     if cfg.winsorize or cfg.standardize:
         mc = 5 if cfg.winsorize else 2 ** 31 - 1
+        # standardize needs the exact clipped moments; otherwise the Gram pivot is the
+        # select kernel's free center (midpoint of the cuts), and no moments pass runs
         cuts = E.select_cuts(panel, cfg.lower_percentile / 100, cfg.upper_percentile / 100, mc,
-                             E.LERP_NUMPY, moments=True)
-        pilot = E.pilot_shift(panel)
-        shift = torch.where(torch.isfinite(cuts.mean), cuts.mean, pilot)
+                             E.LERP_NUMPY, moments=cfg.standardize, center=not cfg.standardize)
         if cfg.standardize:
+            shift = torch.where(torch.isfinite(cuts.mean), cuts.mean, E.pilot_shift(panel))
             inv_scale = 1.0 / cuts.sd
+        else:
+            shift = cuts.center
         if not cfg.winsorize:
             cuts = E.Cuts(torch.full_like(cuts.lo, float("nan")), torch.full_like(cuts.hi, float("nan")),
                           cuts.nvalid, cuts.mean, cuts.sd)

@@ -130,6 +130,34 @@ int fm_select_cuts(const double* cols, int64_t col_stride, int32_t ncols,
                    int32_t lerp_mode, double* lo, double* hi, int32_t* nvalid,
                    double* mean, double* sd, void* stream);
 
+/* fm_select: fm_select_cuts with an argument struct and one more optional output.
+ * Outputs are [ncols][nseg]; every output pointer except lo / hi may be NULL.
+ *   mean, sd: moments of the clipped values (ddof = 1), for the per-month standardization;
+ *   center:   a pivot inside the data for the Gram (midpoint of the cuts, else of the
+ *             segment's finite range, else 0); costs nothing beyond the cuts.
+ * Without a row mask and for segments of <= 6144 rows, passing nvalid enables the
+ * one-wave-per-(segment, column) fast path (nvalid carries its fallback marks). */
+typedef struct fm_select_args {
+    const double* cols;
+    int64_t col_stride;
+    int32_t ncols;
+    const int64_t* seg_off;
+    int32_t nseg;
+    int32_t max_seg_len;
+    const uint8_t* row_mask;     /* [rows] nonzero = row takes part, or NULL */
+    double q_lo, q_hi;           /* quantiles in [0, 1] */
+    int32_t min_count;           /* fewer valid values: cuts are NaN (no clipping) */
+    int32_t lerp_mode;           /* 0 numpy 'linear', 1 pandas groupby.quantile */
+    double* lo;
+    double* hi;
+    int32_t* nvalid;
+    double* mean;
+    double* sd;
+    double* center;
+} fm_select_args;
+
+int fm_select(const fm_select_args* args, void* stream);
+
 int fm_clip(const double* src, double* dst, int64_t col_stride, int32_t ncols,
             const int64_t* seg_off, int32_t nseg, int64_t nrows,
             const double* lo, const double* hi, void* stream);

@@ -56,12 +56,13 @@ def test_percentile_cuts_bit_exact(E):
         assert _same(hi, ref[:, b]), qs[b]
 
 
-def _adversarial_segments(rng):
+def _adversarial_segments(rng, lengths=(1, 2, 3, 5, 10, 50, 63, 64, 65, 255, 256, 257, 1000, 5000,
+                                        12345, 24000)):
     """Month segments that stress the tail fast path and its fallbacks: row-sorted data
     (the thread minima all sit in one wave), heavy ties, constants, infinities, NaNs, and
     lengths around the 256-thread / 64-lane boundaries."""
     segs = []
-    for n in (1, 2, 3, 5, 10, 50, 63, 64, 65, 255, 256, 257, 1000, 5000, 12345, 24000):
+    for n in lengths:
         x = rng.standard_normal(n)
         segs.append(x)
         segs.append(np.sort(x))
@@ -80,9 +81,16 @@ def _adversarial_segments(rng):
     return segs
 
 
-def test_percentile_tails_adversarial(E):
+@pytest.mark.parametrize("wave_path", [False, True])
+def test_percentile_tails_adversarial(E, wave_path):
+    """wave_path: every segment <= 6144 rows, so the wave-per-unit kernel runs first and
+    the workgroup kernel redoes only the units it marks; otherwise the workgroup kernel
+    does everything (a 24000-row segment exceeds the wave kernel's register budget)."""
     rng = np.random.default_rng(7)
-    segs = _adversarial_segments(rng)
+    lengths = (1, 2, 3, 5, 10, 50, 63, 64, 65, 127, 128, 129, 255, 256, 257, 1000, 4999, 5000, 5120,
+               6144) if wave_path else (1, 2, 3, 5, 10, 50, 63, 64, 65, 255, 256, 257, 1000, 5000, 12345,
+                                        24000)
+    segs = _adversarial_segments(rng, lengths)
     vals = np.concatenate(segs)
     labels = np.repeat(np.arange(len(segs)), [len(s) for s in segs])
     panel = E.panel_from_arrays([vals], ["v"], labels)
