@@ -15,6 +15,7 @@
 // statistics, so the interpolated cut is bit-identical to numpy/pandas given the same
 // no-FMA lerp (this file is compiled with -ffp-contract=off).
 #include <math.h>
+#include <stdlib.h>
 
 #include "fm_common.h"
 
@@ -471,18 +472,30 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         select_unit_wg<VPT>(a, blockIdx.x, blockIdx.y, sm);
         return;
     }
+    // Each workgroup scans a contiguous range of units with one coalesced load of the marks
+    // per 256 units (a unit-by-unit scan would pay one memory round trip per unit), then
+    // redoes the marked ones, lowest unit first (each thread clears its own mark).
     const int64_t nunits = (int64_t)a.nseg * a.ncols;
-    for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
-        if (__builtin_amdgcn_readfirstlane(a.nvalid[u]) != -1) continue;   // block-uniform
-        __syncthreads();   // sm is reused across units
-        select_unit_wg<VPT>(a, (int)(u % a.nseg), (int)(u / a.nseg), sm);
+    const int64_t per = (nunits + gridDim.x - 1) / gridDim.x;
+    const int64_t u0 = (int64_t)blockIdx.x * per, u1 = u0 + per < nunits ? u0 + per : nunits;
+    for (int64_t b = u0; b < u1; b += ST) {
+        const int64_t u = b + threadIdx.x;
+        bool mark = u < u1 && a.nvalid[u] == -1;
+        while (true) {
+            const uint64_t pick = block_min_u64<SNW>(mark ? (uint64_t)u : SENT, sm.u64s);
+            if (pick == SENT) break;   // block-uniform
+            if ((uint64_t)u == pick) mark = false;
+            __syncthreads();
+            select_unit_wg<VPT>(a, (int)(pick % a.nseg), (int)(pick / a.nseg), sm);
+            __syncthreads();
+        }
     }
 }
 
 template <int VPT>
 void launch_select(const SelArgs& a, int ncols, hipStream_t st, bool fallback) {
     if (fallback)
-        hipLaunchKernelGGL((select_kernel<VPT, true>), dim3(1024), dim3(ST), 0, st, a);
+        hipLaunchKernelGGL((select_kernel<VPT, true>), dim3(256), dim3(ST), 0, st, a);
     else
         hipLaunchKernelGGL((select_kernel<VPT, false>), dim3(a.nseg, ncols), dim3(ST), 0, st, a);
 }
@@ -501,7 +514,31 @@ void launch_select(const SelArgs& a, int ncols, hipStream_t st, bool fallback) {
 // Units the fast path cannot finish (ranks >= 64, more than 128 candidates, fewer lanes
 // with a valid value than the rank) get nvalid = -1 and are redone by the workgroup
 // kernel's fallback pass.  Results are exact order statistics either way.
-constexpr int WCAP = 128;
+constexpr int WCAP = 256;
+
+// Values at ascending ranks ra <= rb among the c candidates L[0..c) (c <= 64 R), or tau
+// when a rank is >= c (then the order statistic is tau itself, a data value).
+template <int R>
+__device__ __forceinline__ void pick_tail(const double* L, int c, int ra, int rb, double tau, double& va,
+                                          double& vb) {
+    const int lane = lane_id();
+    double v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane + WAVE * r;
+        v[r] = e < c ? L[e] : INFINITY;
+    }
+    wave_sort_f64<R>(v);
+    auto at = [&](int e) -> double {
+        double x = v[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r)
+            if ((e >> 6) == r) x = v[r];   // e is wave-uniform
+        return __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(x), e & 63));
+    };
+    va = ra < c ? at(ra) : tau;
+    vb = rb < c ? at(rb) : tau;
+}
 
 template <int VPL>
 __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
@@ -525,17 +562,21 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
         xv[v] = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
     }
     __builtin_amdgcn_sched_barrier(0);
-    int cnt = 0;
-    double mn = NAN, mx = NAN;
+    // count / min / max with 4 independent accumulators each (the chains would otherwise
+    // serialize on the f64 latency)
+    int cnt4[4] = {0, 0, 0, 0};
+    double mn4[4] = {NAN, NAN, NAN, NAN}, mx4[4] = {NAN, NAN, NAN, NAN};
     const int vfull = L / WAVE;   // rows v < vfull lie inside the segment (wave-uniform)
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
         if (v >= vfull && lane + v * WAVE >= L) xv[v] = NAN;   // past the segment end
-        cnt += isnan(xv[v]) ? 0 : 1;
-        mn = hw_min(mn, xv[v]);   // NaN-ignoring, no canonicalized copy of xv
-        mx = hw_max(mx, xv[v]);
+        cnt4[v & 3] += isnan(xv[v]) ? 0 : 1;
+        mn4[v & 3] = hw_min(mn4[v & 3], xv[v]);   // NaN-ignoring, no canonicalized copy of xv
+        mx4[v & 3] = hw_max(mx4[v & 3], xv[v]);
     }
-    const int n = __builtin_amdgcn_readfirstlane(wave_sum(cnt));
+    const double mn = hw_min(hw_min(mn4[0], mn4[1]), hw_min(mn4[2], mn4[3]));
+    const double mx = hw_max(hw_max(mx4[0], mx4[1]), hw_max(mx4[2], mx4[3]));
+    const int n = __builtin_amdgcn_readfirstlane(wave_sum((cnt4[0] + cnt4[1]) + (cnt4[2] + cnt4[3])));
     double lo = NAN, hi = NAN;
     if (n >= a.min_count && n > 0) {
         int i0, j0, i1, j1;
@@ -550,18 +591,25 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
             // j0-th smallest high word T bounds j0+1 lane minima by key (T << 32 | ~0), so
             // that key is as valid a tau as an exact lane minimum (and s[j0] is a candidate
             // whenever tau is not itself a data value)
-            uint32_t ta[1] = {isnan(mn) ? 0xFFFFFFFFu : (uint32_t)(dkey(mn) >> 32)};
-            uint32_t tb[1] = {isnan(mx) ? 0xFFFFFFFFu : (uint32_t)(~dkey(mx) >> 32)};
+            const uint32_t ha = isnan(mn) ? 0xFFFFFFFFu : (uint32_t)(dkey(mn) >> 32);
+            const uint32_t hb = isnan(mx) ? 0xFFFFFFFFu : (uint32_t)(~dkey(mx) >> 32);
+            uint32_t ta[1] = {ha};
+            uint32_t tb[1] = {hb};
             wave_sort32<1>(ta);
             wave_sort32<1>(tb);
             const uint32_t Ta = (uint32_t)__builtin_amdgcn_readlane((int)ta[0], j0);
             const uint32_t Tb = (uint32_t)__builtin_amdgcn_readlane((int)tb[0], cj);
             ok = Ta != 0xFFFFFFFFu && Tb != 0xFFFFFFFFu;
             if (ok) {
-                double tlo = kval(((uint64_t)Ta << 32) | 0xFFFFFFFFull);
-                double thi = kval(~(((uint64_t)Tb << 32) | 0xFFFFFFFFull));
-                if (isnan(tlo)) tlo = INFINITY;    // high word of +inf's key
-                if (isnan(thi)) thi = -INFINITY;   // high word of -inf's complemented key
+                // tau = the largest lane minimum whose high word is Ta: at least j0+1 lane
+                // minima are <= it, and it is a data value, so ties at tau (e.g. many exact
+                // zeros) stay out of the candidates instead of overflowing them
+                double tlo = ha == Ta ? mn : NAN, thi = hb == Tb ? mx : NAN;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    tlo = hw_max(tlo, __shfl_xor(tlo, o, WAVE));
+                    thi = hw_min(thi, __shfl_xor(thi, o, WAVE));
+                }
                 double* Ll = cbuf[w][0];
                 double* Lh = cbuf[w][1];
                 int clo = 0, chi = 0;   // wave-uniform running counts; overflow is checked once
@@ -587,24 +635,15 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                     // the candidates are never NaN: sort them as doubles (hardware min/max;
                     // equal values, +0 / -0 included, are interchangeable for the result)
-                    double la[2], lb[2];
-#pragma unroll
-                    for (int r = 0; r < 2; ++r) {
-                        const int e = lane + WAVE * r;
-                        la[r] = e < clo ? Ll[e] : INFINITY;
-                        lb[r] = e < chi ? Lh[e] : INFINITY;
+                    if (clo <= 2 * WAVE && chi <= 2 * WAVE) {
+                        pick_tail<2>(Ll, clo, i0, j0, tlo, v0, v1);
+                        pick_tail<2>(Lh, chi, ci, cj, -thi, v3, v2);
+                    } else {   // heavy tails: rare, 256 candidates
+                        pick_tail<4>(Ll, clo, i0, j0, tlo, v0, v1);
+                        pick_tail<4>(Lh, chi, ci, cj, -thi, v3, v2);
                     }
-                    wave_sort_f64<2>(la);
-                    wave_sort_f64<2>(lb);
-                    auto at = [&](const double (&v)[2], int e) -> double {
-                        const uint64_t b = readlane_u64((uint64_t)__double_as_longlong((e >> 6) ? v[1] : v[0]),
-                                                        e & 63);
-                        return __longlong_as_double((long long)b);
-                    };
-                    v0 = i0 < clo ? at(la, i0) : tlo;
-                    v1 = j0 < clo ? at(la, j0) : tlo;
-                    v3 = ci < chi ? -at(lb, ci) : thi;   // rank j1
-                    v2 = cj < chi ? -at(lb, cj) : thi;   // rank i1
+                    v2 = -v2;   // upper tail: candidates were stored negated (ascending)
+                    v3 = -v3;
                 }
             }
         }
@@ -736,6 +775,13 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
         else launch_select_wave<96>(a, st);
         FM_CHECK_LAUNCH("fm_select_cuts(wave)");
     }
+    // diagnostic only (tools/select_marks.py): FM_SELECT_NO_FALLBACK=1 leaves the wave
+    // kernel's fallback marks (nvalid == -1) in place; results are then incomplete
+    static const bool no_fb = [] {
+        const char* e = getenv("FM_SELECT_NO_FALLBACK");
+        return e != nullptr && e[0] == '1';
+    }();
+    if (wave && no_fb) return FM_OK;
     if (vpt <= 2) launch_select<2>(a, ncols, st, wave);
     else if (vpt <= 4) launch_select<4>(a, ncols, st, wave);
     else if (vpt <= 8) launch_select<8>(a, ncols, st, wave);

@@ -94,14 +94,27 @@ __device__ void jacobi_pinv(double* A, double* V, int K, const double* sxy, doub
     }
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    return __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(v), l));
+}
+
+// Per month: bucket sums -> level-cumulative sums (bucket (pattern, u) becomes the sum over
+// levels >= u, so a problem adds one bucket per pattern that contains its model) -> one
+// wave per problem.  The wave keeps the centered moment matrix S over (x_1..x_K, y) in
+// registers, lane i = row i (MD doubles), and factors it by a right-looking Cholesky whose
+// pivot-row broadcasts are readlanes (no LDS round trip per column).  Factoring the
+// augmented matrix [Sxx Sxy; Sxy' Syy] leaves l = L^-1 Sxy in the y row, so the forward
+// substitution comes free; the back substitution L' b = l runs on the transposed factor
+// (one LDS transpose), lane i owning b_i.
 template <int MD>
 __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
     extern __shared__ double bs[];   // [nb][zw(zw+1)/2] packed bucket sums of this month
     __shared__ WaveScratch<MD> ws_all[VNW];
     const int s = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+    const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
     const int zw = a.zw, zz = zw * (zw + 1) / 2;   // packed upper triangle per bucket
-    const int nb = a.npatterns * a.nlevels;
+    const int nl = a.nlevels, npat = a.npatterns, nb = npat * nl;
     const int c0 = a.seg_chunk_off[s], c1 = a.seg_chunk_off[s + 1];
     for (int e = tid; e < nb * zz; e += VT) {
         double acc = 0.0;
@@ -109,145 +122,187 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
         bs[e] = acc;
     }
     __syncthreads();
+    for (int e = tid; e < npat * zz; e += VT) {
+        const int pid = e / zz, f = e - pid * zz;
+        double* b0 = bs + (int64_t)pid * nl * zz + f;
+        double run = b0[(nl - 1) * zz];
+        for (int l = nl - 2; l >= 0; --l) {
+            run += b0[l * zz];
+            b0[l * zz] = run;
+        }
+    }
+    __syncthreads();
     WaveScratch<MD>& ws = ws_all[w];
     const int rs = a.pmax + 2;
+    constexpr int PKW = MD * (MD + 1) / 2;   // packed entries of one problem Gram
+    constexpr int EPL = (PKW + WAVE - 1) / WAVE;
     for (int p = w; p < a.nprob; p += VNW) {
         const int m = a.prob_model[p], u = a.prob_level[p], nz = a.prob_nz[p];
         const int* zi = a.prob_z + p * 32;
-        const int K = nz - 2;
-        // ---- assemble the problem Gram G[i][j] over its buckets
-        for (int e = lane; e < nz * nz; e += WAVE) {
-            const int i = e / nz, j = e - (e / nz) * nz;
-            const int zr = zi[i] < zi[j] ? zi[i] : zi[j], zc = zi[i] < zi[j] ? zi[j] : zi[i];
-            const int off = zr * zw - (zr * (zr - 1)) / 2 + (zc - zr);
-            double acc = 0.0;
-            for (int b = 0; b < nb; ++b) {
-                const int pid = b / a.nlevels, lvl = b - pid * a.nlevels;
-                if (((a.pattern_models[pid] >> m) & 1u) && lvl >= u) acc += bs[b * zz + off];
+        const int K = nz - 2, K1 = K + 1;
+        // ---- the problem's Gram G[i][j] (i, j < nz over its z indices) into the wave's V:
+        // lanes over packed (i <= j) entries, patterns in the outer loop, so each pattern
+        // costs one batch of independent LDS reads; G is written in both triangles
+        int off[EPL], dst[EPL], dsw[EPL];
+        double acc[EPL];
+#pragma unroll
+        for (int t = 0; t < EPL; ++t) {
+            const int e = lane + WAVE * t;
+            int i = 0, rem = e;   // packed index e -> (i, j), rows of length nz - i
+            while (i < nz && rem >= nz - i) {
+                rem -= nz - i;
+                ++i;
             }
-            ws.A[i * MD + j] = acc;
+            const bool in = i < nz;
+            const int j = in ? i + rem : 0;
+            const int zr = in ? zi[i] : 0, zc = in ? zi[j] : 0;
+            const int r = zr < zc ? zr : zc, c = zr < zc ? zc : zr;
+            off[t] = in ? r * zw - (r * (r - 1)) / 2 + (c - r) : 0;
+            dst[t] = in ? i * MD + j : -1;
+            dsw[t] = in ? j * MD + i : -1;
+            acc[t] = 0.0;
         }
+        for (int q = 0; q < npat; ++q) {
+            if (!((a.pattern_models[q] >> m) & 1u)) continue;   // wave-uniform
+            const double* bq = bs + (q * nl + u) * zz;
+#pragma unroll
+            for (int t = 0; t < EPL; ++t) acc[t] += bq[off[t]];
+        }
+#pragma unroll
+        for (int t = 0; t < EPL; ++t)
+            if (dst[t] >= 0) {
+                ws.V[dst[t]] = acc[t];
+                ws.V[dsw[t]] = acc[t];
+            }
         wave_sync();
-        const double n = ws.A[0];
+        const double* Gp = ws.V;   // G[i][j], row stride MD; z index 0 is the intercept
+        const int zl = lane < K1 ? zi[1 + lane] : 0;   // panel z index of this lane's row
+        const int li = lane < K1 ? 1 + lane : 0;       // this lane's row in Gp
+        const double n = Gp[0];
+        const double g0 = lane < K1 ? Gp[li] : 0.0;    // first moment of this lane's variable
+        const double gdiag = lane < K1 ? Gp[li * MD + li] : 0.0;
         const int64_t ro = ((int64_t)s * a.nprob + p) * rs;
         uint32_t st = 0;
-        // inf in the problem's rows (statsmodels MissingDataError / pinv(X)@y = +-inf): a
-        // regressor or y value of +-inf makes its Gram diagonal entry sum(z^2) = +inf (the
-        // z of a finite value stays finite; entries of columns the problem does not use,
-        // which may hold NaN / inf garbage, are never read here)
-        {
-            bool infx = false, infy = false;
-            if (lane >= 1 && lane < nz) {
-                const bool d = isinf(ws.A[lane * MD + lane]);
-                infx = d && lane <= K;
-                infy = d && lane == K + 1;
-            }
-            if (__ballot(infx) != 0) st |= FM_ST_INF_IN_X;
-            if (__ballot(infy) != 0) st |= FM_ST_INF_IN_Y;
-        }
+        // inf in the problem's rows: a regressor or y value of +-inf makes its Gram diagonal
+        // sum(z^2) = +inf (columns the problem does not use are never read)
+        if (__ballot(lane < K && isinf(gdiag)) != 0) st |= FM_ST_INF_IN_X;
+        if (__ballot(lane == K && isinf(gdiag)) != 0) st |= FM_ST_INF_IN_Y;
         if (a.gram_flags) st |= a.gram_flags[(int64_t)s * a.nmodels + m] & (FM_ST_INF_IN_X | FM_ST_INF_IN_Y);
         if (!(n >= (double)(K + 1))) {
             for (int k = lane; k < rs; k += WAVE) a.rec[ro + k] = k == a.pmax + 1 ? n : NAN;
             if (lane == 0) a.status[(int64_t)s * a.nprob + p] = FM_ST_SKIPPED;
-            wave_sync();
             continue;
         }
-        // ---- centered moments S over (x_1..x_K, y)
-        const int K1 = K + 1;
-        for (int e = lane; e < K1 * K1; e += WAVE) {
-            const int i = e / K1, j = e - (e / K1) * K1;
-            ws.V[i * MD + j] = ws.A[(1 + i) * MD + 1 + j] - ws.A[1 + i] * ws.A[1 + j] / n;
+        // ---- centered moments: row i of S, S[i][j] = G(z_i, z_j) - G(0, z_i) G(0, z_j) / n
+        double row[MD];
+        double sii = 0.0, sxy = 0.0;   // S[i][i], S[i][K] of this lane
+#pragma unroll
+        for (int j = 0; j < MD; ++j) {
+            row[j] = 0.0;
+            if (j < K1) {
+                const double v = lane < K1 ? Gp[li * MD + 1 + j] - g0 * Gp[1 + j] / n : 0.0;
+                row[j] = v;
+                if (j == lane) sii = v;
+                if (j == K) sxy = v;
+            }
         }
-        if (lane < K1) ws.mu[lane] = ws.A[1 + lane] / n;
-        if (lane < K) ws.sdiag[lane] = ws.A[(1 + lane) * MD + 1 + lane];
-        wave_sync();
-        if (lane < K) ws.sxy[lane] = ws.V[lane * MD + K];
+        const double mu = g0 / n;
         if (a.moments) {
             double* mo = a.moments + ((int64_t)s * a.nprob + p) * a.mom_stride;
             if (lane == 0) mo[0] = n;
-            if (lane < K1) mo[1 + lane] = ws.mu[lane];
-            for (int e = lane; e < K1 * K1; e += WAVE)
-                mo[1 + K1 + e] = ws.V[(e / K1) * MD + (e - (e / K1) * K1)];
+            if (lane < K1) {
+                mo[1 + lane] = mu;
+#pragma unroll
+                for (int j = 0; j < MD; ++j)
+                    if (j < K1) mo[1 + K1 + lane * K1 + j] = row[j];
+            }
         }
-        const double syy = ws.V[K * MD + K];
         if ((a.prob_flags[p] & 1) != 0) {
-            bool sus = false;
-            if (lane < K) sus = !(ws.V[lane * MD + lane] > 1e-10 * ws.sdiag[lane]);
-            if (__ballot(sus) != 0) st |= FM_ST_CONST_SUSPECT;
+            if (__ballot(lane < K && !(sii > 1e-10 * gdiag)) != 0) st |= FM_ST_CONST_SUSPECT;
         }
-        // ---- Cholesky of Sxx (in A), lanes over the trailing-update entries
-        for (int e = lane; e < K * K; e += WAVE) {
-            const int i = e / K, j = e - (e / K) * K;
-            ws.A[i * MD + j] = ws.V[i * MD + j];
-        }
-        wave_sync();
+        const double syy = readlane_f64(sii, K);
+        // ---- augmented Cholesky, lane i = row i; rows >= K1 are zero
         bool ok = true;
-        for (int k = 0; k < K; ++k) {
-            const double piv = ws.A[k * MD + k];
-            const double orig = ws.V[k * MD + k];
-            if (!(orig > 0.0) || !(piv > CHOL_REL * orig)) {
-                ok = false;
-                break;
+#pragma unroll
+        for (int k = 0; k < MD - 1; ++k) {
+            if (ok && k < K) {   // wave-uniform
+                const double orig = readlane_f64(sii, k);
+                const double piv = readlane_f64(row[k], k);
+                if (!(orig > 0.0) || !(piv > CHOL_REL * orig)) {
+                    ok = false;
+                } else {
+                    const double lkk = sqrt(piv);
+                    const double rinv = 1.0 / lkk;
+                    const double lik = row[k] * rinv;
+#pragma unroll
+                    for (int j = k + 1; j < MD; ++j) {
+                        if (j <= K) {
+                            const double sj = readlane_f64(row[j], k) * rinv;   // L[j][k]
+                            row[j] -= lik * sj;
+                        }
+                    }
+                    row[k] = lane == k ? lkk : lik;
+                }
             }
-            const double lkk = sqrt(piv);
-            wave_sync();
-            if (lane > k && lane < K) ws.A[lane * MD + k] /= lkk;
-            if (lane == k) ws.A[k * MD + k] = lkk;
-            wave_sync();
-            const int mrem = K - k - 1;
-            for (int e = lane; e < mrem * mrem; e += WAVE) {
-                const int i = k + 1 + e / mrem, j = k + 1 + (e - (e / mrem) * mrem);
-                if (j <= i) ws.A[i * MD + j] -= ws.A[i * MD + k] * ws.A[j * MD + k];
-            }
-            wave_sync();
         }
         double bi = 0.0;
         if (ok) {
-            // L y = Sxy then L' b = y, lane i owns row i (values broadcast by shuffles)
-            bi = lane < K ? ws.sxy[lane] : 0.0;
-            for (int j = 0; j < K; ++j) {
-                if (lane == j) bi = bi / ws.A[j * MD + j];
-                const double yj = __shfl(bi, j, WAVE);
-                if (lane > j && lane < K) bi -= ws.A[lane * MD + j] * yj;
+            // transpose through LDS: lane i then holds column i of L (and l_i)
+            double* T = ws.A;
+#pragma unroll
+            for (int j = 0; j < MD; ++j)
+                if (lane < K1) T[lane * MD + j] = row[j];
+            wave_sync();
+            double col[MD];
+#pragma unroll
+            for (int r = 0; r < MD; ++r) col[r] = lane < MD ? T[r * MD + (lane & (MD - 1))] : 0.0;
+            double t = lane < K ? T[K * MD + lane] : 0.0;   // l_i
+#pragma unroll
+            for (int j = MD - 2; j >= 0; --j) {
+                if (j < K) {
+                    const double bj = readlane_f64(t, j) / readlane_f64(col[j], j);
+                    if (lane == j) t = bj;
+                    else if (lane < j) t -= col[j] * bj;
+                }
             }
-            for (int j = K - 1; j >= 0; --j) {
-                if (lane == j) bi = bi / ws.A[j * MD + j];
-                const double xj = __shfl(bi, j, WAVE);
-                if (lane < j) bi -= ws.A[j * MD + lane] * xj;
-            }
+            bi = lane < K ? t : 0.0;
+            wave_sync();
         } else {
             st |= FM_ST_RANK_DEF;
-            for (int e = lane; e < K * K; e += WAVE) {
-                const int i = e / K, j = e - (e / K) * K;
-                ws.A[i * MD + j] = ws.V[i * MD + j];
-            }
+            // rebuild Sxx (rows were overwritten) for the pseudo-inverse fallback
+#pragma unroll
+            for (int j = 0; j < MD; ++j)
+                if (j < K && lane < K) ws.A[lane * MD + j] = Gp[li * MD + 1 + j] - g0 * Gp[1 + j] / n;
+            if (lane < K) ws.sxy[lane] = sxy;
             wave_sync();
             if (lane == 0) jacobi_pinv<MD>(ws.A, ws.V, K, ws.sxy, ws.b);
             wave_sync();
             bi = lane < K ? ws.b[lane] : 0.0;
+            wave_sync();
         }
         // R^2 = 1 - SSR/SST (centered), raw-coordinate intercept
-        double t_sxy = lane < K ? bi * ws.sxy[lane] : 0.0;
-        double t_mu = lane < K ? bi * ws.mu[lane] : 0.0;
+        double t_sxy = lane < K ? bi * sxy : 0.0;
+        double t_mu = lane < K ? bi * mu : 0.0;
         double t_ab = 0.0;
-        if (a.add_back && lane < K) t_ab = bi * a.add_back[(int64_t)(zi[1 + lane] - 1) * a.nseg + s];
+        if (a.add_back && lane < K) t_ab = bi * a.add_back[(int64_t)(zl - 1) * a.nseg + s];
         t_sxy = wave_sum(t_sxy);
         t_mu = wave_sum(t_mu);
         t_ab = wave_sum(t_ab);
         const double r2 = 1.0 - (syy - t_sxy) / syy;
-        double icpt = ws.mu[K] - t_mu;
+        double icpt = readlane_f64(mu, K) - t_mu;
         if (a.add_back) icpt += a.add_back[(int64_t)(zi[K + 1] - 1) * a.nseg + s] - t_ab;
+        // b_{k-1} to lane k (all lanes active: a bpermute reads nothing from inactive lanes);
+        // rs <= 34 < 64, so lane k writes record entry k
+        const double bsh = __shfl(bi, lane > 0 ? lane - 1 : 0, WAVE);
         for (int k = lane; k < rs; k += WAVE) {
-            double v = NAN;
+            double v = NAN;   // pad between the slopes and R^2
             if (k == 0) v = icpt;
+            else if (k <= K) v = bsh;
             else if (k == a.pmax) v = r2;
             else if (k == a.pmax + 1) v = n;
             a.rec[ro + k] = v;
         }
-        wave_sync();
-        if (lane < K) a.rec[ro + 1 + lane] = bi;
         if (lane == 0) a.status[(int64_t)s * a.nprob + p] = st | FM_ST_FITTED;
-        wave_sync();
     }
 }
 

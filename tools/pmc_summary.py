@@ -15,7 +15,7 @@ def main():
         meta[d] = (r["Kernel_Name"], int(float(r.get("Grid_Size", 0) or 0)))
     groups = defaultdict(list)
     for d, (name, g) in meta.items():
-        short = name.split("(")[0][-60:]
+        short = name.split("(")[0].split("<")[0][-40:] + ("<" + name.split("<")[1].split(">")[0] + ">" if "<" in name else "")
         if pats and not any(p in name for p in pats):
             continue
         groups[(short, g)].append(d)
