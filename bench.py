@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--cpu-months", type=int, default=240, help="oracle CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify one step against the oracle")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
     return ap.parse_args()
 
 
@@ -68,52 +69,117 @@ def main():
     seg_lo, seg_hi = rank * T_loc, (rank + 1) * T_loc
     counts = [T_loc] * world
 
-    def step():
+    # One step = three device phases (each replayed from a HIP graph: the pass is ~20 short
+    # kernels, so eager launches would leave the GPU waiting on the host) with the two RCCL
+    # exchanges of the month-sharded path between them, into static buffers.
+    rec_g = st_g = None
+
+    def phase_local():
         res, names, cuts, level, bp = LW.local_stage(panel, cfg, model_cols)
+        return res
+
+    def phase_ts(res):
+        gres = res
         if world > 1:
-            rec_g, st_g = D.gather_records(res.rec, res.status, counts)
             gres = E.FMResult(problems=res.problems, rec=rec_g, status=st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
-        else:
-            gres = res
         ix, summ, roll, pred, pst = LW.time_series_stage(gres, cfg, moments=res.moments,
                                                          seg_lo=seg_lo, seg_hi=seg_hi)
-        if world > 1:
-            pred, pst = D.combine_predictive(pred, pst)
+        return gres, summ, pred, pst
+
+    def phase_pred(pred, pst):
         psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
-        return gres, summ, psumm
+        return psumm
+
+    def exchange_records(res):
+        if world > 1:
+            D.gather_records_into(res.rec, res.status, rec_g, st_g)
+
+    def exchange_pred(pred, pst):
+        if world > 1:
+            D.combine_predictive(pred, pst)
+
+    def step_eager():
+        res = phase_local()
+        exchange_records(res)
+        gres, summ, pred, pst = phase_ts(res)
+        exchange_pred(pred, pst)
+        return gres, summ, phase_pred(pred, pst)
 
     for _ in range(args.warmup):
+        res0 = phase_local()
+        if world > 1 and rec_g is None:
+            rec_g = torch.empty((T_glob,) + tuple(res0.rec.shape[1:]), dtype=res0.rec.dtype, device=dev)
+            st_g = torch.empty((T_glob,) + tuple(res0.status.shape[1:]), dtype=res0.status.dtype, device=dev)
+        exchange_records(res0)
+        g0, s0, p0, ps0 = phase_ts(res0)
+        exchange_pred(p0, ps0)
+        phase_pred(p0, ps0)
+    torch.cuda.synchronize()
+
+    graphs = None
+    if not args.no_graph:
+        # capture (on a side stream, as torch.cuda.graph requires); eager warmup has filled
+        # every host-side cache, so the captured launches are exactly a step's kernels
+        ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga):
+            res_s = phase_local()
+        exchange_records(res_s)
+        with torch.cuda.graph(gb):
+            gres_s, summ_s, pred_s, pst_s = phase_ts(res_s)
+        exchange_pred(pred_s, pst_s)
+        with torch.cuda.graph(gc):
+            psumm_s = phase_pred(pred_s, pst_s)
+        graphs = (ga, gb, gc)
+
+        def step():
+            ga.replay()
+            exchange_records(res_s)
+            gb.replay()
+            exchange_pred(pred_s, pst_s)
+            gc.replay()
+            return gres_s, summ_s, psumm_s
+    else:
+        step = step_eager
+
+    for _ in range(2):
         step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    timer = E.KernelTimer()
-    with timer:
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
-        torch.cuda.synchronize()
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
     if world > 1:
         dt = D.max_over_ranks(dt, dev)
+    # per-kernel device times (HIP events on the launch stream), from eager steps outside
+    # the timed region: they feed the roofline of the dominant kernel
+    timer = E.KernelTimer()
+    with timer:
+        for _ in range(max(3, min(args.steps, 10))):
+            step_eager()
+    torch.cuda.synchronize()
     gres, summ, psumm = out
     nfit = int(((gres.status & 1) != 0).sum().item())
 
-    # roofline of the dominant kernel (per-launch algorithmic bytes / avg launch time)
+    # roofline of the dominant kernel: per-launch algorithmic bytes / its device time, the
+    # latter from the latest launch re-issued back to back (E.time_launch: no launch gaps)
     C = panel.ncols
     kern = {}
     for tag in timer.names():
-        kern[tag] = timer.avg_ms(tag)
+        kern[tag] = timer.avg_ms(tag)   # events around each eager launch (incl. launch gaps)
+    dev_ms = {t: E.time_launch(t) for t in ("fm_select_cuts", "fm_gram", "fm_solve")}
     bytes_select = rows_local * C * 8            # one read of every winsorized column
     bytes_gram = rows_local * (C * 8 + 1)         # every column + the universe level byte
     cand = {"fm_select_cuts": bytes_select, "fm_gram": bytes_gram}
-    dom = max(cand, key=lambda k: kern.get(k, 0.0))
-    dom_ms = kern[dom]
+    dom = max(cand, key=lambda k: dev_ms[k])
+    dom_ms = dev_ms[dom]
     achieved = cand[dom] / (dom_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -147,7 +213,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_launch": cand[dom], "avg_launch_ms": dom_ms},
-        "kernel_ms": {k: round(v, 4) for k, v in kern.items()},
+        "kernel_ms": {k: round(v, 4) for k, v in dev_ms.items()},
+        "kernel_ms_eager_events": {k: round(v, 4) for k, v in kern.items()},
+        "graph": not args.no_graph,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(panel, args, LW)

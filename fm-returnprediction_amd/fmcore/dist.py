@@ -49,6 +49,22 @@ def gather_records(rec, status, counts, group=None):
     return _gather_rows(rec, counts, group), _gather_rows(status, counts, group)
 
 
+def gather_records_into(rec, status, rec_out, status_out, counts=None, group=None):
+    """gather_records into preallocated global buffers (static addresses, so the stages
+    around the exchange can be replayed from HIP graphs).  Equal month counts per rank use
+    one all_gather_into_tensor per buffer."""
+    world = dist.get_world_size(group)
+    if counts is None or len(set(counts)) == 1:
+        dist.all_gather_into_tensor(rec_out, rec.contiguous(), group=group)
+        dist.all_gather_into_tensor(status_out, status.contiguous(), group=group)
+    else:
+        r, s = gather_records(rec, status, counts, group)
+        rec_out.copy_(r)
+        status_out.copy_(s)
+    assert rec_out.shape[0] == (rec.shape[0] * world if counts is None else sum(counts))
+    return rec_out, status_out
+
+
 def combine_predictive(pred, pst, group=None):
     """Rows of other ranks' months are zero in `pred`/`pst`: a SUM all-reduce merges them
     (each compact row has exactly one owner)."""

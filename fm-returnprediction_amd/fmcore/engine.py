@@ -65,6 +65,32 @@ class KernelTimer:
 
 _TIMER = None
 
+# The latest argument struct of each struct-taking entry point, with the tensors it points
+# to kept alive, so one kernel can be re-issued in isolation (time_launch).
+LAST_LAUNCH = {}
+
+
+def _remember(tag, name, struct, *keep):
+    LAST_LAUNCH[tag] = (name, struct, keep)
+
+
+def time_launch(tag, reps=20):
+    """Average device milliseconds of the latest `tag` launch, re-issued `reps` times back
+    to back on the current stream.  The host stays ahead of the device, so unlike events
+    around single launches of a host-bound pipeline this excludes launch gaps.  The
+    re-issued launches rewrite the same outputs with the same values."""
+    name, struct, keep = LAST_LAUNCH[tag]
+    st = _stream()
+    L.call(name, L.C.byref(struct), st)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        L.call(name, L.C.byref(struct), st)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
 
 def _kcall(tag, name, *args):
     t = _TIMER
@@ -208,6 +234,7 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
                       q_hi=float(q_hi), min_count=int(min_count), lerp_mode=int(mode), lo=lo.data_ptr(),
                       hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=_ptr(mean), sd=_ptr(sd), center=_ptr(cen))
     _kcall(tag, "fm_select", L.C.byref(sa), _stream())
+    _remember(tag, "fm_select", sa, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off)
     return Cuts(lo, hi, nv, mean, sd, cen)
 
 
@@ -459,7 +486,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
     nprob = len(problems)
     rs = pmax + 2
     rec = torch.empty((T, nprob, rs), dtype=torch.float64, device=dev)
-    status = torch.zeros((T, nprob), dtype=torch.int32, device=dev)
+    status = torch.empty((T, nprob), dtype=torch.int32, device=dev)   # every problem is in one group
     mom_stride = 1 + (pmax + 1) + (pmax + 1) ** 2
     mom = torch.empty((T, nprob, mom_stride), dtype=torch.float64, device=dev) if moments else None
     plan = _chunk_plan(panel)
@@ -469,7 +496,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
     for gpl in groups:
         nb = gpl.npatterns * nlevels
         partial = torch.empty((plan.nchunks, nb, zw * (zw + 1) // 2), dtype=torch.float64, device=dev)
-        flags = torch.zeros((T, gpl.nmodels), dtype=torch.int32, device=dev)
+        flags = torch.empty((T, gpl.nmodels), dtype=torch.int32, device=dev)   # reserved: never read
         ga = L.GramArgs(
             cols=src.data_ptr(), col_stride=src.stride(0), ncols=ncols, nseg=T,
             seg_off=panel.seg_off.data_ptr(), chunk_seg=plan.chunk_seg.data_ptr(),
@@ -479,6 +506,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
             model_ymask=gpl.ym.data_ptr(), nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(),
             npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr())
         _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
+        _remember("fm_gram", "fm_gram", ga, src, partial, flags, lo, hi, shift, inv_scale, level, plan, gpl)
         ng = gpl.nprob
         grec = torch.empty((T, ng, rs), dtype=torch.float64, device=dev)
         gst = torch.empty((T, ng), dtype=torch.int32, device=dev)   # the solve writes every entry
@@ -489,9 +517,10 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
             nlevels=nlevels, npatterns=gpl.npatterns, pattern_models=gpl.patm.data_ptr(), nprob=ng,
             prob_model=gpl.pm.data_ptr(), prob_level=gpl.pl.data_ptr(), prob_z=gpl.pz.data_ptr(),
             prob_nz=gpl.pnz.data_ptr(), prob_flags=gpl.pf.data_ptr(), add_back=_ptr(add_back),
-            gram_flags=flags.data_ptr(), nmodels=gpl.nmodels, pmax=pmax, rec=grec.data_ptr(),
+            gram_flags=None, nmodels=gpl.nmodels, pmax=pmax, rec=grec.data_ptr(),
             status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride)
         _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
+        _remember("fm_solve", "fm_solve", sa, partial, plan, gpl, add_back, flags, grec, gst, gmom)
         # inf in y: statsmodels' pinv(X) @ y gives +-inf / NaN coefficients.  The fix-up scans
         # the status on the device (npairs = -1), so there is no host round trip.
         _kcall("fm_inf_y_fix", "fm_inf_y_fix", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
