@@ -105,11 +105,38 @@ def build_models(panel: E.DevicePanel, model_cols: Dict[str, List[str]], y="retx
     return models, names
 
 
+_SIDE = {}
+
+
+def _side_stream(device):
+    s = _SIDE.get(str(device))
+    if s is None:
+        s = _SIDE[str(device)] = torch.cuda.Stream(device=device)
+    return s
+
+
 def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx"):
     """Panel-sized work for one shard of months: cuts, universes, batched Gram + solve."""
     cuts = None
     shift = None
     inv_scale = None
+    # The NYSE breakpoints (600 latency-bound units) run on a side stream, concurrently with
+    # the bandwidth-bound winsorize cuts; the Gram waits for both (a fork/join that HIP graph
+    # capture records as two parallel branches).
+    level, bp = None, None
+    nlevels = 1
+    main = torch.cuda.current_stream()
+    side = None
+    if cfg.universes:
+        side = _side_stream(main.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            a, b = E.nyse_breakpoints(panel)
+            level = E.universe_level(panel, a, b)
+        for t in (a, b, level):
+            t.record_stream(main)
+        nlevels = 3
+        bp = (a, b)
     if cfg.winsorize or cfg.standardize:
         mc = 5 if cfg.winsorize else 2 ** 31 - 1
         # standardize needs the exact clipped moments; otherwise the Gram pivot is the
@@ -124,13 +151,8 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
         if not cfg.winsorize:
             cuts = E.Cuts(torch.full_like(cuts.lo, float("nan")), torch.full_like(cuts.hi, float("nan")),
                           cuts.nvalid, cuts.mean, cuts.sd)
-    level, bp = None, None
-    nlevels = 1
-    if cfg.universes:
-        a, b = E.nyse_breakpoints(panel)
-        level = E.universe_level(panel, a, b)
-        nlevels = 3
-        bp = (a, b)
+    if side is not None:
+        main.wait_stream(side)
     models, names = build_models(panel, model_cols, y=y, fig1=cfg.fig1, universes=cfg.universes)
     res = E.fm_pass(panel, models, level=level, nlevels=nlevels, cuts=cuts, shift=shift,
                     inv_scale=inv_scale, add_back=None if cfg.standardize else shift,
