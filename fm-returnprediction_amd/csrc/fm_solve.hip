@@ -16,6 +16,8 @@
 // chunks into LDS, then the waves take the month's problems round-robin.
 #include <math.h>
 
+#include <type_traits>
+
 #include "fm_common.h"
 
 namespace fm {
@@ -306,6 +308,244 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// zw == 16 (<= 15 panel columns): four problems per wave.  A problem owns one 16-lane row of
+// the wave and lane i holds row i of its Gram (row 0 = the intercept, rows 1..K+1 = the
+// centered moments S of x_1..x_K, y), so the pivot-row broadcasts of the Cholesky are DPP
+// row_newbcast moves (VALU modifiers: no LDS round trip, no readlane hazards) and four
+// factorizations run in the time of one.  Rank-deficient problems (rare) take the Jacobi
+// pseudo-inverse path one at a time.
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+template <int L>
+__device__ __forceinline__ int rowbc_i(int v) {   // lane L of this lane's 16-lane row
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + L, 0xF, 0xF, false);
+}
+template <int L>
+__device__ __forceinline__ double rowbc(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)rowbc_i<L>((int)(uint32_t)b), hi = (uint32_t)rowbc_i<L>((int)(uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double rowsum(double v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+    return v;
+}
+
+constexpr int G16 = 16;   // lanes per problem
+
+__global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
+    extern __shared__ double bs[];   // [nb][136] packed bucket sums of this month
+    // per wave: four transpose tiles, or (afterwards, one problem at a time) the Jacobi
+    // fallback's scratch; the union keeps three workgroups per CU (all months resident)
+    constexpr int TT = G16 * (G16 + 1);
+    static_assert(sizeof(WaveScratch<16>) <= 4 * TT * sizeof(double), "scratch union");
+    __shared__ double wsc[VNW][4 * TT];
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+    const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
+    constexpr int zw = 16, zz = 136;
+    const int nl = a.nlevels, npat = a.npatterns, nb = npat * nl;
+    const int c0 = a.seg_chunk_off[s], c1 = a.seg_chunk_off[s + 1];
+    for (int e = tid; e < nb * zz; e += VT) {
+        double acc = 0.0;
+        for (int c = c0; c < c1; ++c) acc += a.partial[(int64_t)c * nb * zz + e];
+        bs[e] = acc;
+    }
+    __syncthreads();
+    for (int e = tid; e < npat * zz; e += VT) {   // level-cumulative buckets
+        const int pid = e / zz, f = e - pid * zz;
+        double* b0 = bs + (int64_t)pid * nl * zz + f;
+        double run = b0[(nl - 1) * zz];
+        for (int l = nl - 2; l >= 0; --l) {
+            run += b0[l * zz];
+            b0[l * zz] = run;
+        }
+    }
+    __syncthreads();
+    const int g = lane >> 4, i = lane & 15;
+    const int rs = a.pmax + 2;
+    double* T = wsc[w] + g * TT;
+    for (int p0 = w * 4; p0 < a.nprob; p0 += VNW * 4) {
+        const int p = p0 + g;
+        const bool live = p < a.nprob;
+        const int pp = live ? p : p0;
+        const int m = a.prob_model[pp], u = a.prob_level[pp], nz = a.prob_nz[pp];
+        const int K = nz - 2, K1 = K + 1;
+        const int zi = i < nz ? a.prob_z[pp * 32 + i] : 0;   // z index of this lane's row
+        // ---- row i of the problem Gram: one level-cumulative bucket per pattern with m
+        int off[G16];
+        static_for<0, G16>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const int zj = rowbc_i<j>(zi);
+            const int r = zi < zj ? zi : zj, c = zi < zj ? zj : zi;
+            off[j] = r * zw - (r * (r - 1)) / 2 + (c - r);
+        });
+        double G[G16];
+#pragma unroll
+        for (int j = 0; j < G16; ++j) G[j] = 0.0;
+        for (int q = 0; q < npat; ++q) {
+            if (!((a.pattern_models[q] >> m) & 1u)) continue;   // per problem
+            const double* bq = bs + (q * nl + u) * zz;
+#pragma unroll
+            for (int j = 0; j < G16; ++j) G[j] += bq[off[j]];
+        }
+        const double n = rowbc<0>(G[0]);
+        // centered moments: lane i (1 <= i <= K1) holds S row r = i - 1, S[r][c] in row[c]
+        const bool srow = i >= 1 && i <= K1;
+        double row[G16];
+        double sii = 0.0, sxy = 0.0, gdiag = 0.0;
+        static_for<0, G16>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if (i == j) gdiag = G[j];
+            if constexpr (j + 1 < G16) {
+                const double g0j = rowbc<0>(G[j + 1]);   // G[0][j+1]
+                const double v = srow && j < K1 ? G[j + 1] - G[0] * g0j / n : 0.0;
+                row[j] = v;
+                if (i == j + 1) sii = v;
+                if (j == K) sxy = v;
+            } else {
+                row[j] = 0.0;
+            }
+        });
+        const double mu = G[0] / n;   // lane i: mean of its variable
+        const uint64_t gm = 0xFFFFull << (16 * g);
+        uint32_t st = 0;
+        if ((__ballot(i >= 1 && i <= K && isinf(gdiag)) & gm) != 0) st |= FM_ST_INF_IN_X;
+        if ((__ballot(i == K1 && isinf(gdiag)) & gm) != 0) st |= FM_ST_INF_IN_Y;
+        const int64_t ro = ((int64_t)s * a.nprob + pp) * rs;
+        const bool skip = !(n >= (double)(K + 1));
+        if (live && skip) {
+            for (int k = i; k < rs; k += G16) a.rec[ro + k] = k == a.pmax + 1 ? n : NAN;
+            if (i == 0) a.status[(int64_t)s * a.nprob + pp] = FM_ST_SKIPPED;
+        }
+        const bool act0 = live && !skip;
+        if (act0 && a.moments) {
+            double* mo = a.moments + ((int64_t)s * a.nprob + pp) * a.mom_stride;
+            if (i == 0) mo[0] = n;
+            if (srow) {
+                mo[i] = mu;   // mo[1 + r]
+#pragma unroll
+                for (int c = 0; c < G16 - 1; ++c)
+                    if (c < K1) mo[1 + K1 + (i - 1) * K1 + c] = row[c];
+            }
+        }
+        if (act0 && (a.prob_flags[pp] & 1) != 0) {
+            if ((__ballot(i >= 1 && i <= K && !(sii > 1e-10 * gdiag)) & gm) != 0) st |= FM_ST_CONST_SUSPECT;
+        }
+        // ---- augmented Cholesky of S (pivot r = k sits in lane k + 1)
+        bool ok = act0;
+        static_for<0, G16 - 1>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const bool act = ok && k < K;
+            const double orig = rowbc<k + 1>(sii);
+            const double piv = rowbc<k + 1>(row[k]);
+            const bool bad = act && (!(orig > 0.0) || !(piv > CHOL_REL * orig));
+            if (bad) ok = false;
+            const bool go = act && !bad;
+            const double lkk = sqrt(piv);
+            const double rinv = 1.0 / lkk;
+            const double lik = row[k] * rinv;
+            static_for<k + 1, G16>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                const double sj = rowbc<k + 1>(row[j]) * rinv;   // L[j][k] = S(k)[k][j] / lkk
+                if (go && j <= K) row[j] -= lik * sj;
+            });
+            if (go) row[k] = i == k + 1 ? lkk : lik;
+        });
+        // lanes of a live, unskipped problem with a collapsed pivot: rank deficient
+        const bool rank_def = act0 && !ok;
+        // ---- back substitution L' b = l on the transposed factor: lane i then holds
+        // column r = i - 1 of L (col[c] = L[c][r]) and t = l_r
+        if (srow) {
+#pragma unroll
+            for (int c = 0; c < G16; ++c) T[(i - 1) * (G16 + 1) + c] = row[c];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double col[G16];
+        const int rr = i >= 1 ? i - 1 : 0;
+#pragma unroll
+        for (int c = 0; c < G16 - 1; ++c) col[c] = T[c * (G16 + 1) + rr];
+        col[G16 - 1] = 0.0;
+        double t = (i >= 1 && i <= K) ? T[K * (G16 + 1) + rr] : 0.0;
+        static_for<0, G16 - 1>([&](auto jc) {
+            constexpr int j = 14 - decltype(jc)::value;   // descending
+            const double bj = rowbc<j + 1>(t) / rowbc<j + 1>(col[j]);
+            if (ok && j < K) {
+                if (i == j + 1) t = bj;
+                else if (i >= 1 && i - 1 < j) t -= col[j] * bj;
+            }
+        });
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double bi = (ok && i >= 1 && i <= K) ? t : 0.0;   // slope of x_{i-1}
+        // ---- rank-deficient problems of this wave: Jacobi pseudo-inverse, one at a time
+        const uint64_t rd = __ballot(rank_def && i == 0);
+        for (uint64_t q = rd; q; q &= q - 1) {
+            const int gq = __builtin_ctzll(q) >> 4;   // wave-uniform
+            WaveScratch<16>& J = *reinterpret_cast<WaveScratch<16>*>(wsc[w]);
+            const int Kq = __shfl(K, gq * 16, WAVE);
+            // rebuild Sxx (rows were overwritten) from G, the shuffles with every lane active
+            {
+                double g0c[G16 - 1];
+#pragma unroll
+                for (int c = 0; c < G16 - 1; ++c) g0c[c] = __shfl(G[c + 1], gq * 16, WAVE);
+                const double nq = __shfl(n, gq * 16, WAVE);
+                if (g == gq && i >= 1 && i <= Kq) {
+#pragma unroll
+                    for (int c = 0; c < G16 - 1; ++c)
+                        if (c < Kq) J.A[(i - 1) * 16 + c] = G[c + 1] - G[0] * g0c[c] / nq;
+                    J.sxy[i - 1] = sxy;
+                }
+            }
+            wave_sync();
+            if (lane == 0) jacobi_pinv<16>(J.A, J.V, Kq, J.sxy, J.b);
+            wave_sync();
+            if (g == gq && i >= 1 && i <= Kq) bi = J.b[i - 1];
+            wave_sync();
+        }
+        if (rank_def) st |= FM_ST_RANK_DEF;
+        // ---- R^2 = 1 - SSR/SST (centered), raw-coordinate intercept
+        const bool xl = i >= 1 && i <= K;
+        double t_sxy = xl ? bi * sxy : 0.0;
+        double t_mu = xl ? bi * mu : 0.0;
+        double t_ab = 0.0;
+        if (a.add_back && xl && act0) t_ab = bi * a.add_back[(int64_t)(zi - 1) * a.nseg + s];
+        t_sxy = rowsum(t_sxy);
+        t_mu = rowsum(t_mu);
+        t_ab = rowsum(t_ab);
+        const double syy = __shfl(sii, g * 16 + (K1 < 16 ? K1 : 15), WAVE);   // S[K][K]
+        const double muy = __shfl(mu, g * 16 + (K1 < 16 ? K1 : 15), WAVE);
+        const double r2 = 1.0 - (syy - t_sxy) / syy;
+        double icpt = muy - t_mu;
+        if (a.add_back && act0) {
+            const int zy = a.prob_z[pp * 32 + K + 1];
+            icpt += a.add_back[(int64_t)(zy - 1) * a.nseg + s] - t_ab;
+        }
+        if (act0) {
+            for (int k = i; k < rs; k += G16) {
+                double v = NAN;   // pad between the slopes and R^2
+                if (k == 0) v = icpt;
+                else if (k <= K) v = k == i ? bi : NAN;   // k == i on the first pass
+                else if (k == a.pmax) v = r2;
+                else if (k == a.pmax + 1) v = n;
+                a.rec[ro + k] = v;
+            }
+            if (i == 0) a.status[(int64_t)s * a.nprob + pp] = st | FM_ST_FITTED;
+        }
+    }
+}
+
 // Exact nonzero-constant test for problems flagged CONST_SUSPECT (statsmodels
 // add_constant(has_constant='skip'): np.ptp(x)==0 & all(x != 0), src/regressions.py:50).
 __global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t stride, int ncols,
@@ -527,14 +767,14 @@ extern "C" int fm_solve(const fm_solve_args* args, void* stream) {
     const size_t dyn = (size_t)a.npatterns * a.nlevels * (a.zw * (a.zw + 1) / 2) * sizeof(double);
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)solve_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)solve16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             MAXB_LDS * (int)sizeof(double));
         (void)hipFuncSetAttribute((const void*)solve_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             MAXB_LDS * (int)sizeof(double));
         attr_set = true;
     }
     if (a.zw == 16)
-        hipLaunchKernelGGL(solve_kernel<16>, dim3(a.nseg), dim3(VT), dyn, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(solve16_kernel, dim3(a.nseg), dim3(VT), dyn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(solve_kernel<32>, dim3(a.nseg), dim3(VT), dyn, (hipStream_t)stream, a);
     FM_CHECK_LAUNCH("fm_solve");
