@@ -287,3 +287,306 @@ extern "C" int fm_predictive(const double* moments, int32_t mom_stride, int32_t 
     FM_CHECK_LAUNCH("fm_predictive");
     return FM_OK;
 }
+
+// ---------------------------------------------------------------------------------------
+// fm_ts_fused: the whole time-series stage in one launch.  Grid (kmax + nchunk, nprob):
+//   x <  kmax   summary workgroup of coefficient k: dropna, mean, Newey-West (fm_ts_summary)
+//   x >= kmax   rolling workgroup of RROWS consecutive fitted-month rows: the rolling means
+//               of every coefficient on those rows (fm_rolling_mean) and, from the rows'
+//               `lag`-earlier rolling means, their predictive slopes (fm_predictive)
+// Every workgroup first rebuilds its problem's fitted-month list (fm_ts_compact) in LDS --
+// a few hundred status words, cheaper than a kernel boundary -- and works on LDS copies of
+// the records it needs, so no phase waits on a dependent chain of L2 gathers.  Called on the
+// predictive records (roll = pred = NULL) it gives their summary.
+namespace fm {
+namespace {
+
+constexpr int FT = 256;
+constexpr int FNW = FT / WAVE;
+constexpr int RROWS = 64;    // rows per rolling workgroup (4 predictive rows per wave pass)
+constexpr int RPIECE = 8;    // rolling outputs per task: one direct window sum, then slides
+constexpr int MAXL = 8;      // Newey-West lags accumulated in one sweep
+
+__host__ __device__ __forceinline__ size_t ts_ix_bytes(int T) { return ((size_t)T * 4 + 15) & ~(size_t)15; }
+
+// fitted months of problem p, ascending, into ixs; returns their count (block-uniform)
+__device__ __forceinline__ int ts_compact_lds(const fm_ts_args& a, int p, int* ixs, int* wtot) {
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+    int base = 0;
+    for (int s0 = 0; s0 < a.nseg; s0 += FT) {
+        const int s = s0 + tid;
+        const bool f = s < a.nseg && (a.status[(int64_t)s * a.s_seg + (int64_t)p * a.s_prob] & FM_ST_FITTED);
+        const uint64_t bm = __ballot(f);
+        if (lane == 0) wtot[w] = (int)__popcll(bm);
+        __syncthreads();
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int q = 0; q < FNW; ++q) {
+            const int c = wtot[q];
+            off += q < w ? c : 0;
+            tot += c;
+        }
+        if (f) ixs[base + off + mask_rank(bm)] = s;
+        base += tot;
+        __syncthreads();
+    }
+    return base;
+}
+
+__device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs, int cnt, double* xs,
+                              int* wtot, double* dred) {
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+    const double* rk = a.rec + (int64_t)p * a.r_prob + k;
+    for (int i = tid; i < cnt; i += FT) xs[i] = rk[(int64_t)ixs[i] * a.r_seg];   // all in flight
+    __syncthreads();
+    // dropna in place, month order kept (each pass reads its span before any write lands)
+    int n = 0;
+    for (int i0 = 0; i0 < cnt; i0 += FT) {
+        const int i = i0 + tid;
+        const double x = i < cnt ? xs[i] : NAN;
+        const bool v = !isnan(x);
+        const uint64_t bm = __ballot(v);
+        if (lane == 0) wtot[w] = (int)__popcll(bm);
+        __syncthreads();
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int q = 0; q < FNW; ++q) {
+            const int c = wtot[q];
+            off += q < w ? c : 0;
+            tot += c;
+        }
+        if (v) xs[n + off + mask_rank(bm)] = x;
+        n += tot;
+        __syncthreads();
+    }
+    double sum = 0.0;
+    for (int i = tid; i < n; i += FT) sum += xs[i];
+    sum = block_sum<FNW>(sum, dred);
+    const double mu = n > 0 ? sum / (double)n : NAN;
+    // gamma_0 .. gamma_min(lags, MAXL) in one sweep, one reduction
+    const int lags = a.nw_lags < MAXL ? a.nw_lags : MAXL;
+    double gl[MAXL + 1];
+#pragma unroll
+    for (int L = 0; L <= MAXL; ++L) gl[L] = 0.0;
+    for (int i = tid; i < n; i += FT) {
+        const double ui = xs[i] - mu;
+#pragma unroll
+        for (int L = 0; L <= MAXL; ++L)
+            if (L <= lags && i >= L) gl[L] += ui * (xs[i - L] - mu);
+    }
+    __syncthreads();   // block_sum's readers are done with dred
+#pragma unroll
+    for (int L = 0; L <= MAXL; ++L) {
+        const double v = wave_sum(gl[L]);
+        if (lane == 0) dred[L * FNW + w] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int L = 0; L <= MAXL; ++L) {
+        double t = 0.0;
+#pragma unroll
+        for (int q = 0; q < FNW; ++q) t += dred[L * FNW + q];
+        gl[L] = t;
+    }
+    __syncthreads();
+    double acc = 0.0;
+    for (int L = 1; L <= a.nw_lags; ++L) {
+        const double wgt = 1.0 - ((double)L / (double)n);
+        if (wgt < 0.0) break;
+        double gk = 0.0;
+        if (L <= MAXL) {
+#pragma unroll
+            for (int q = 1; q <= MAXL; ++q)
+                if (q == L) gk = gl[q];
+        } else {
+            for (int i = L + tid; i < n; i += FT) gk += (xs[i] - mu) * (xs[i - L] - mu);
+            gk = block_sum<FNW>(gk, dred);
+        }
+        acc += wgt * gk;
+    }
+    if (tid == 0) {
+        const int64_t o = (int64_t)p * a.kmax + k;
+        double se = NAN;
+        if (n >= 2) se = sqrt((gl[0] + 2.0 * acc) / ((double)n * (double)n));
+        a.mean[o] = mu;
+        a.se[o] = se;
+        a.tstat[o] = mu / se;
+        a.nobs[o] = n;
+    }
+}
+
+__device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* ixs, int cnt,
+                              double* lds_d) {
+    const int tid = threadIdx.x;
+    const int r0 = chunk * RROWS;
+    if (r0 >= cnt) return;                               // block-uniform
+    const int r1 = r0 + RROWS < cnt ? r0 + RROWS : cnt;
+    const int T = a.nseg, PM = a.pmax;
+    const bool predictive = a.pred != nullptr;
+    const int q0 = predictive ? (r0 - a.lag > 0 ? r0 - a.lag : 0) : r0;   // rows rolled here
+    const int j0 = q0 - a.window + 1 > 0 ? q0 - a.window + 1 : 0;          // rows read
+    const int nsrc = r1 - j0, nq = r1 - q0;
+    double* xs = lds_d;                  // [nsrc][PM]
+    double* rl = lds_d + nsrc * PM;      // [nq][PM]
+    const double* rp = a.rec + (int64_t)p * a.r_prob;
+    for (int e = tid; e < nsrc * PM; e += FT) {
+        const int j = e / PM, k = e - j * PM;
+        xs[e] = rp[(int64_t)ixs[j0 + j] * a.r_seg + k];
+    }
+    __syncthreads();
+    const int npc = (nq + RPIECE - 1) / RPIECE;
+    for (int task = tid; task < PM * npc; task += FT) {
+        const int k = task / npc, i0 = q0 + (task - k * npc) * RPIECE;
+        const int i1 = i0 + RPIECE < r1 ? i0 + RPIECE : r1;
+        double sm = 0.0;
+        int c = 0;
+        for (int j = (i0 - a.window + 1 > 0 ? i0 - a.window + 1 : 0); j <= i0; ++j) {
+            const double x = xs[(j - j0) * PM + k];
+            if (!isnan(x)) {
+                sm += x;
+                ++c;
+            }
+        }
+        for (int i = i0; i < i1; ++i) {
+            if (i > i0) {
+                const double x = xs[(i - j0) * PM + k];
+                if (!isnan(x)) {
+                    sm += x;
+                    ++c;
+                }
+                const int jo = i - a.window;
+                if (jo >= 0) {
+                    const double y = xs[(jo - j0) * PM + k];
+                    if (!isnan(y)) {
+                        sm -= y;
+                        --c;
+                    }
+                }
+            }
+            const double m = c >= a.min_periods ? sm / (double)c : NAN;
+            rl[(i - q0) * PM + k] = m;
+            if (i >= r0) a.roll[((int64_t)p * T + i) * PM + k] = m;
+        }
+    }
+    if (!predictive) return;
+    __syncthreads();
+    // predictive slopes: a 16-lane group per row, lane b owns column b of each S row
+    const int K = a.prob_k[p], K1 = K + 1;
+    const int g = tid >> 4, b = tid & 15;
+    for (int i = r0 + g; i < r0 + RROWS; i += FT / 16) {     // uniform trip count (shuffles)
+        const bool row = i < r1;
+        const int s = row ? ixs[i] : -1;
+        const bool mine = row && s >= a.seg_lo && s < a.seg_hi;
+        bool ok = false;
+        double n = NAN, tb = 0.0, ty = 0.0, syy = NAN;
+        if (mine && i >= a.lag) {
+            const double* c = rl + (i - a.lag - q0) * PM;
+            bool bad = false;
+            for (int q = 0; q <= K; ++q) bad |= isnan(c[q]);
+            const double* mo = a.moments + ((int64_t)(s - a.seg_lo) * a.nprob + p) * a.mom_stride;
+            n = mo[0];
+            ok = !bad && n >= 2.0;
+            if (ok) {
+                const double* S = mo + 1 + K1;
+                syy = S[K * K1 + K];
+                for (int bb = b; bb <= K; bb += 16) {
+                    const double cb = bb < K ? c[1 + bb] : 0.0;
+#pragma unroll 4
+                    for (int r = 0; r < K; ++r) {
+                        const double v = S[r * K1 + bb] * c[1 + r];
+                        if (bb < K) tb += v * cb;
+                        else ty += v;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 8; m >= 1; m >>= 1) {
+            tb += __shfl_xor(tb, m, 16);
+            ty += __shfl_xor(ty, m, 16);
+        }
+        if (row && b == 0) {
+            double* o = a.pred + ((int64_t)p * T + i) * 4;
+            uint32_t st = 0;
+            double slope = NAN, r2 = NAN, nn = NAN;
+            if (!mine) {
+                // another rank's month (sharded runs): zero record for the sum-combine
+                slope = r2 = nn = 0.0;
+            } else if (ok) {
+                slope = ty / tb;
+                r2 = (ty * ty) / (tb * syy);
+                nn = n;
+                st = FM_ST_FITTED;
+                if (!(tb > 0.0)) st |= FM_ST_CONST_COL;
+            }
+            o[0] = slope;
+            o[1] = r2;
+            o[2] = nn;
+            o[3] = 0.0;
+            a.pred_status[(int64_t)p * T + i] = st;
+        }
+    }
+}
+
+__global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {
+    extern __shared__ double lds[];
+    __shared__ int wtot[FNW];
+    __shared__ double dred[(MAXL + 1) * FNW];
+    const int p = blockIdx.y, bx = blockIdx.x;
+    int* ixs = reinterpret_cast<int*>(lds);
+    double* lds_d = lds + ts_ix_bytes(a.nseg) / 8;
+    const int cnt = ts_compact_lds(a, p, ixs, wtot);
+    if (bx == 0) {
+        for (int i = threadIdx.x; i < cnt; i += FT) a.idx[(int64_t)p * a.nseg + i] = ixs[i];
+        if (threadIdx.x == 0) a.count[p] = cnt;
+    }
+    if (bx < a.kmax) ts_summary_wg(a, p, bx, ixs, cnt, lds_d, wtot, dred);
+    else ts_rolling_wg(a, p, bx - a.kmax, ixs, cnt, lds_d);
+}
+
+}  // namespace
+}  // namespace fm
+
+extern "C" size_t fm_ts_fused_lds_bytes(int32_t nseg, int32_t pmax, int32_t window, int32_t lag,
+                                         int32_t rolling, int32_t predictive) {
+    using namespace fm;
+    size_t d = (size_t)nseg * 8;
+    if (rolling) {
+        const size_t l = predictive ? (size_t)lag : 0;
+        const size_t r = (size_t)pmax * 8 * ((RROWS + l + (size_t)window - 1) + (RROWS + l));
+        d = d > r ? d : r;
+    }
+    return ts_ix_bytes(nseg) + d;
+}
+
+extern "C" int fm_ts_fused(const fm_ts_args* args, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(args != nullptr, "fm_ts_fused: null args");
+    const fm_ts_args& a = *args;
+    FM_REQUIRE(a.rec && a.status && a.idx && a.count && a.mean && a.se && a.tstat && a.nobs,
+               "fm_ts_fused: null pointer");
+    FM_REQUIRE(a.nw_lags >= 0, "fm_ts_fused: nw_lags < 0");
+    FM_REQUIRE(a.roll == nullptr || (a.window >= 1 && a.min_periods >= 0 && a.pmax >= 1),
+               "fm_ts_fused: bad rolling window");
+    FM_REQUIRE(a.pred == nullptr || (a.roll && a.moments && a.prob_k && a.pred_status && a.lag >= 1),
+               "fm_ts_fused: the predictive stage needs roll, moments, prob_k, pst and lag >= 1");
+    if (a.nprob == 0 || a.nseg == 0) return FM_OK;
+    const size_t lds = fm_ts_fused_lds_bytes(a.nseg, a.pmax, a.window, a.lag, a.roll != nullptr,
+                                             a.pred != nullptr);
+    FM_REQUIRE(lds <= FM_TS_FUSED_MAX_LDS,
+               "fm_ts_fused: series too long for LDS staging (use the per-stage entry points)");
+    if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit: opt in (once)
+        static bool attr_set = false;
+        if (!attr_set) {
+            FM_REQUIRE(hipFuncSetAttribute((const void*)ts_fused_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           FM_TS_FUSED_MAX_LDS) == hipSuccess,
+                       "fm_ts_fused: cannot raise the dynamic LDS limit");
+            attr_set = true;
+        }
+    }
+    const int nchunk = a.roll ? (a.nseg + RROWS - 1) / RROWS : 0;
+    hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk, a.nprob), dim3(FT), lds, (hipStream_t)stream, a);
+    FM_CHECK_LAUNCH("fm_ts_fused");
+    return FM_OK;
+}

@@ -24,6 +24,7 @@ FM_ST_RANK_DEF = 0x40
 FM_MAX_COLS = 31
 FM_MAX_MODELS = 6
 FM_MAX_LEVELS = 3
+FM_TS_FUSED_MAX_LDS = 128 * 1024
 
 _p = C.c_void_p
 _i32 = C.c_int32
@@ -49,6 +50,17 @@ class SelectArgs(C.Structure):
         ("max_seg_len", _i32), ("row_mask", _p), ("q_lo", _f64), ("q_hi", _f64),
         ("min_count", _i32), ("lerp_mode", _i32), ("lo", _p), ("hi", _p), ("nvalid", _p),
         ("mean", _p), ("sd", _p), ("center", _p),
+    ]
+
+
+class TsArgs(C.Structure):
+    _fields_ = [
+        ("rec", _p), ("r_seg", _i64), ("r_prob", _i64), ("status", _p), ("s_seg", _i64),
+        ("s_prob", _i64), ("nseg", _i32), ("nprob", _i32), ("kmax", _i32), ("nw_lags", _i32),
+        ("idx", _p), ("count", _p), ("mean", _p), ("se", _p), ("tstat", _p), ("nobs", _p),
+        ("work", _p), ("window", _i32), ("min_periods", _i32), ("pmax", _i32), ("roll", _p),
+        ("moments", _p), ("mom_stride", _i32), ("prob_k", _p), ("lag", _i32), ("seg_lo", _i32),
+        ("seg_hi", _i32), ("pred", _p), ("pred_status", _p),
     ]
 
 
@@ -88,6 +100,8 @@ _SIGS = {
     "fm_rolling_mean": (_i32, [_p, _i64, _i64, _p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "fm_predictive": (_i32, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p,
                              _p]),
+    "fm_ts_fused": (_i32, [C.POINTER(TsArgs), _p]),
+    "fm_ts_fused_lds_bytes": (C.c_size_t, [_i32, _i32, _i32, _i32, _i32, _i32]),
     "fm_forecast": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p]),
     "fm_segment_moments": (_i32, [_p, _i64, _i32, _p, _i32, _p, _i32, _i32, _p, _p, _p, _p]),
     "fm_distinct_count": (_i32, [_p, _i64, _p, _i64, _i32, _p, _i32, _i32, _i64, _i64, _p, _p, _p]),

@@ -632,8 +632,71 @@ def predictive_result(res: FMResult, ix: TSIndex, roll, lag=1, seg_lo=0, seg_hi=
 
 def summarize_predictive(pred, pst, nw_lags=4):
     P, T, _ = pred.shape
-    ix = ts_compact(pst, 1, T, T, P)
-    return ts_summary(pred, 4, T * 4, ix, T, P, 3, nw_lags), ix
+    if not ts_fused_fits(T):
+        ix = ts_compact(pst, 1, T, T, P)
+        return ts_summary(pred, 4, T * 4, ix, T, P, 3, nw_lags), ix
+    ix, summ, _, _, _ = ts_fused(pred, 4, T * 4, pst, 1, T, T, P, 3, nw_lags)
+    return summ, ix
+
+
+def ts_fused_fits(nseg, pmax=0, window=None, lag=1, predictive=False):
+    """Whether fm_ts_fused can stage this series in LDS (else the per-stage kernels run)."""
+    need = L.load().fm_ts_fused_lds_bytes(nseg, pmax, window or 0, lag, int(window is not None),
+                                           int(bool(predictive)))
+    return need <= L.FM_TS_FUSED_MAX_LDS
+
+
+def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_lags=4,
+             window=None, min_periods=None, pmax=None, moments=None, mom_stride=0, prob_k=None,
+             lag=1, seg_lo=0, seg_hi=None, predictive=False):
+    """The whole time-series stage in one launch (fm_ts_fused): TSIndex, Summary and, when
+    ``window`` is given, the rolling means [P, T, pmax]; with ``predictive`` also the
+    predictive records [P, T, 4] and status [P, T]."""
+    dev = rec.device
+    idx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
+    cnt = torch.empty(nprob, dtype=torch.int32, device=dev)
+    mean = torch.empty((nprob, kmax), dtype=torch.float64, device=dev)
+    se, ts = torch.empty_like(mean), torch.empty_like(mean)
+    nobs = torch.empty((nprob, kmax), dtype=torch.int32, device=dev)
+    roll = pred = pst = None
+    if window is not None:
+        roll = torch.empty((nprob, nseg, pmax), dtype=torch.float64, device=dev)
+    if predictive:
+        pred = torch.empty((nprob, nseg, 4), dtype=torch.float64, device=dev)
+        pst = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
+    ta = L.TsArgs(rec=rec.data_ptr(), r_seg=r_seg, r_prob=r_prob, status=status.data_ptr(), s_seg=s_seg,
+                  s_prob=s_prob, nseg=nseg, nprob=nprob, kmax=kmax, nw_lags=nw_lags, idx=idx.data_ptr(),
+                  count=cnt.data_ptr(), mean=mean.data_ptr(), se=se.data_ptr(), tstat=ts.data_ptr(),
+                  nobs=nobs.data_ptr(), work=None, window=window or 0,
+                  min_periods=min_periods or 0, pmax=pmax or 0, roll=_ptr(roll), moments=_ptr(moments),
+                  mom_stride=mom_stride, prob_k=_ptr(prob_k), lag=lag, seg_lo=seg_lo,
+                  seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst))
+    _kcall("fm_ts_fused", "fm_ts_fused", L.C.byref(ta), _stream())
+    _remember("fm_ts_fused", "fm_ts_fused", ta, rec, status, idx, cnt, mean, se, ts, nobs, roll,
+              moments, prob_k, pred, pst)
+    return TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst
+
+
+def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag=1, seg_lo=0,
+                       seg_hi=None, moments=None, rolling=True, predictive=True):
+    """compact_result + summarize_result + rolling_result + predictive_result in one launch."""
+    T, P, rs = res.rec.shape
+    mom = res.moments if moments is None else moments
+    window = window if (rolling or predictive) else None
+    if not ts_fused_fits(T, res.pmax, window, lag, predictive):
+        ix = compact_result(res)
+        summ, _ = summarize_result(res, ix, nw_lags)
+        roll = pred = pst = None
+        if window is not None:
+            roll = rolling_result(res, ix, window, min_periods)
+        if predictive:
+            pred, pst = predictive_result(res, ix, roll, lag, seg_lo, seg_hi, moments)
+        return ix, summ, roll, pred, pst
+    pk = _small_tensor(tuple(p.K for p in res.problems), torch.int32, res.rec.device) if predictive else None
+    return ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
+                    window=window, min_periods=min_periods,
+                    pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
+                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive)
 
 
 def forecast(panel: DevicePanel, coef, cols=None):

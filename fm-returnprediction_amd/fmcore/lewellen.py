@@ -161,14 +161,10 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
 
 
 def time_series_stage(res: E.FMResult, cfg: PipelineConfig, moments=None, seg_lo=0, seg_hi=None):
-    ix = E.compact_result(res)
-    summ, _ = E.summarize_result(res, ix, cfg.nw_lags)
-    roll = pred = pst = psumm = None
-    if cfg.forecasts or cfg.fig1:
-        roll = E.rolling_result(res, ix, cfg.window, cfg.min_periods)
-    if cfg.forecasts:
-        pred, pst = E.predictive_result(res, ix, roll, cfg.lag, seg_lo=seg_lo, seg_hi=seg_hi,
-                                        moments=moments)
+    # one launch (fm_ts_fused): compaction, FM summaries, rolling means, predictive slopes
+    ix, summ, roll, pred, pst = E.time_series_result(
+        res, cfg.nw_lags, cfg.window, cfg.min_periods, cfg.lag, seg_lo=seg_lo, seg_hi=seg_hi,
+        moments=moments, rolling=cfg.forecasts or cfg.fig1, predictive=cfg.forecasts)
     return ix, summ, roll, pred, pst
 
 

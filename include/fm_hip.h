@@ -210,6 +210,42 @@ int fm_predictive(const double* moments, int32_t mom_stride, int32_t nseg, int32
                   const double* rolling, int32_t pmax, int32_t lag, int32_t seg_lo,
                   int32_t seg_hi, double* pred, uint32_t* pred_status, void* stream);
 
+/* fm_ts_fused: fm_ts_compact + fm_ts_summary + fm_rolling_mean + fm_predictive in one
+ * launch (per problem: a workgroup per coefficient summary and per 64 fitted-month rows of
+ * rolling means + predictive slopes, each staging its records in LDS).  roll == NULL skips
+ * the rolling and predictive phases, pred == NULL the predictive phase; called on the
+ * predictive records (rec = pred, status = pred_status) it gives their FM summary.  Outputs
+ * as in the separate entry points; work is unused (may be NULL). */
+typedef struct fm_ts_args {
+    const double* rec;            /* records, element (month s, problem p, k) at s*r_seg + p*r_prob + k */
+    int64_t r_seg, r_prob;
+    const uint32_t* status;       /* status of (s, p) at s*s_seg + p*s_prob */
+    int64_t s_seg, s_prob;
+    int32_t nseg, nprob, kmax, nw_lags;
+    int32_t* idx;                 /* [nprob][nseg] fitted months, ascending */
+    int32_t* count;               /* [nprob] */
+    double* mean;                 /* [nprob][kmax] */
+    double* se;
+    double* tstat;
+    int32_t* nobs;
+    double* work;                 /* unused (ABI slot), may be NULL */
+    int32_t window, min_periods, pmax;
+    double* roll;                 /* [nprob][nseg][pmax] or NULL */
+    const double* moments;        /* [seg_hi - seg_lo][nprob][mom_stride] */
+    int32_t mom_stride;
+    const int32_t* prob_k;        /* [nprob] */
+    int32_t lag, seg_lo, seg_hi;
+    double* pred;                 /* [nprob][nseg][4] or NULL */
+    uint32_t* pred_status;        /* [nprob][nseg] */
+} fm_ts_args;
+
+/* LDS bytes the fused launch stages per workgroup; it must not exceed FM_TS_FUSED_MAX_LDS
+ * (otherwise use fm_ts_compact / fm_ts_summary / fm_rolling_mean / fm_predictive). */
+#define FM_TS_FUSED_MAX_LDS (128 * 1024)
+size_t fm_ts_fused_lds_bytes(int32_t nseg, int32_t pmax, int32_t window, int32_t lag,
+                             int32_t rolling, int32_t predictive);
+int fm_ts_fused(const fm_ts_args* args, void* stream);
+
 int fm_forecast(const double* cols, int64_t col_stride, int32_t K, const int64_t* seg_off,
                 int32_t nseg, int64_t nrows, const double* coef, int32_t coef_stride,
                 double* out, void* stream);

@@ -278,8 +278,11 @@ def test_mid_panel_golden(R):
 
 
 # ---------------------------------------------------------------- full pipeline vs oracle
-def test_pipeline_vs_oracle(E):
+@pytest.mark.parametrize("fused", [True, False], ids=["ts_fused", "ts_per_stage"])
+def test_pipeline_vs_oracle(E, fused, monkeypatch):
     from fmcore import lewellen as LW, synth
+    if not fused:   # the per-stage kernels that serve series too long for LDS staging
+        monkeypatch.setattr(E, "ts_fused_fits", lambda *a, **k: False)
     T, N = 150, 400
     a = synth.synth_arrays(T, N, 99, nan_rate=0.03, present_rate=0.9)
     cols = list(dict.fromkeys(["retx"] + [c for xs in LW.table2_models().values() for c in xs] + LW.FIG1_VARS))
