@@ -121,24 +121,37 @@ def main():
     if not args.no_graph:
         # capture (on a side stream, as torch.cuda.graph requires); eager warmup has filled
         # every host-side cache, so the captured launches are exactly a step's kernels
-        ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(ga):
-            res_s = phase_local()
-        exchange_records(res_s)
-        with torch.cuda.graph(gb):
-            gres_s, summ_s, pred_s, pst_s = phase_ts(res_s)
-        exchange_pred(pred_s, pst_s)
-        with torch.cuda.graph(gc):
-            psumm_s = phase_pred(pred_s, pst_s)
-        graphs = (ga, gb, gc)
+        if world == 1:
+            # no exchange at N=1: the whole step is one graph (no inter-graph launch gaps)
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                res_s = phase_local()
+                gres_s, summ_s, pred_s, pst_s = phase_ts(res_s)
+                psumm_s = phase_pred(pred_s, pst_s)
+            graphs = (g1,)
 
-        def step():
-            ga.replay()
+            def step():
+                g1.replay()
+                return gres_s, summ_s, psumm_s
+        else:
+            ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                res_s = phase_local()
             exchange_records(res_s)
-            gb.replay()
+            with torch.cuda.graph(gb):
+                gres_s, summ_s, pred_s, pst_s = phase_ts(res_s)
             exchange_pred(pred_s, pst_s)
-            gc.replay()
-            return gres_s, summ_s, psumm_s
+            with torch.cuda.graph(gc):
+                psumm_s = phase_pred(pred_s, pst_s)
+            graphs = (ga, gb, gc)
+
+            def step():
+                ga.replay()
+                exchange_records(res_s)
+                gb.replay()
+                exchange_pred(pred_s, pst_s)
+                gc.replay()
+                return gres_s, summ_s, psumm_s
     else:
         step = step_eager
 
