@@ -10,6 +10,9 @@
  *   fm_select_cuts  <- np.percentile(vals, 1/99) per month per var
  *                      (src/calc_Lewellen_2014.py:519-523) and pandas
  *                      groupby("mthcaldt")["me"].quantile([.2,.5]) over NYSE rows (:74-82)
+ *   fm_select       <- the same, struct-argument form: wave-per-(month, column) tail
+ *                      selection with an exact workgroup fallback, plus the Gram pivot
+ *                      `center` (the Table-2 fast path; fm_select_cuts calls it)
  *   fm_clip         <- subdf[var].clip(lower, upper) (src/calc_Lewellen_2014.py:524)
  *   fm_standardize  <- per-month z-score (north-star extension; no reference line)
  *   fm_universe_level <- me >= me_20 / me >= me_50 masks (src/calc_Lewellen_2014.py:95-96)
@@ -29,6 +32,8 @@
  *                      (src/calc_Lewellen_2014.py:926)
  *   fm_predictive   <- build-defined extension: lagged-rolling-coefficient forecasts and
  *                      predictive-slope regressions (paper Table 3; no reference line)
+ *   fm_ts_fused     <- fm_ts_compact + fm_ts_summary + fm_rolling_mean + fm_predictive in
+ *                      one launch (src/regressions.py:78-131; src/calc_Lewellen_2014.py:926)
  *   fm_forecast     <- build-defined extension A7: per-row F = a_{t-1} + b_{t-1}'x_t
  *   fm_segment_moments, fm_distinct_count <- build_table_1's monthly mean / std(ddof=1)
  *                      and permno nunique (src/calc_Lewellen_2014.py:623-646)
