@@ -48,6 +48,48 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Value of lane (this lane ^ J), without LDS: DPP quad_perm (1, 2), two bank-masked DPP
+// row rotations (4), DPP row_ror:8 (8), v_permlane16_swap / v_permlane32_swap (16, 32).
+// Verified against __shfl_xor by tools/probes/xor_probe.hip.
+template <int J>
+__device__ __forceinline__ uint32_t xor_lanes(uint32_t x) {
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0xB1, 0xF, 0xF, false);
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x4E, 0xF, 0xF, false);
+    } else if constexpr (J == 4) {
+        const int t = __builtin_amdgcn_update_dpp((int)x, (int)x, 0x12C, 0xF, 0x5, false);   // lanes 0-3, 8-11
+        return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)x, 0x124, 0xF, 0xA, false);    // lanes 4-7, 12-15
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xF, 0xF, false);
+    } else if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (__lane_id() & 16) ? r[0] : r[1];
+    } else {
+        static_assert(J == 32, "xor_lanes: J in {1,2,4,8,16,32}");
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (__lane_id() & 32) ? r[0] : r[1];
+    }
+}
+// run-time J that is a constant after unrolling (the switch folds away)
+__device__ __forceinline__ uint32_t xor_lanes_u32(uint32_t x, int j) {
+    switch (j) {
+        case 1: return xor_lanes<1>(x);
+        case 2: return xor_lanes<2>(x);
+        case 4: return xor_lanes<4>(x);
+        case 8: return xor_lanes<8>(x);
+        case 16: return xor_lanes<16>(x);
+        default: return xor_lanes<32>(x);
+    }
+}
+__device__ __forceinline__ uint64_t xor_lanes_u64(uint64_t x, int j) {
+    const uint32_t lo = xor_lanes_u32((uint32_t)x, j), hi = xor_lanes_u32((uint32_t)(x >> 32), j);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double xor_lanes_f64(double x, int j) {
+    return __longlong_as_double((long long)xor_lanes_u64((uint64_t)__double_as_longlong(x), j));
+}
+
 // Hardware v_max_f64 / v_min_f64 (IEEE mode: a quiet-NaN operand yields the other one).
 // Inline asm, because the maxnum/minnum lowering canonicalizes its inputs first: an extra
 // v_max_f64 per operand, and a second register copy of every value kept for later use.

@@ -139,7 +139,7 @@ __device__ __forceinline__ void radix_pair(const double (&xv)[VPT], int ri, int 
 }
 
 // Bitonic sort (ascending) of the 64*R keys held by one wave: element e = lane + 64*r lives
-// in register r of lane e&63.  Cross-lane stages exchange through ds_bpermute; the j=64
+// in register r of lane e&63.  Cross-lane stages exchange through DPP / permlane; the j=64
 // stage of R=2 is register-local.
 template <int R>
 __device__ __forceinline__ void wave_sort(uint64_t (&v)[R]) {
@@ -162,7 +162,7 @@ __device__ __forceinline__ void wave_sort(uint64_t (&v)[R]) {
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const uint64_t p = (uint64_t)__shfl_xor((long long)v[r], j, WAVE);
+                    const uint64_t p = xor_lanes_u64(v[r], j);
                     const bool up = (((lane + WAVE * r) & k) == 0);
                     const bool lower = (lane & j) == 0;
                     const bool take_min = lower == up;
@@ -175,7 +175,9 @@ __device__ __forceinline__ void wave_sort(uint64_t (&v)[R]) {
 }
 
 // Non-NaN doubles (element e = lane + 64 r in register r): bitonic sort ascending with the
-// hardware min / max (no 64-bit integer compares and selects).
+// hardware min / max (no 64-bit integer compares and selects).  Cross-lane stages exchange
+// through DPP / permlane swaps (no LDS round trip); both min and max are computed and the
+// lane's role selects one (inline asm is convergent: a conditional one becomes a branch).
 template <int R>
 __device__ __forceinline__ void wave_sort_f64(double (&v)[R]) {
     const int lane = lane_id();
@@ -196,18 +198,19 @@ __device__ __forceinline__ void wave_sort_f64(double (&v)[R]) {
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const double p = __shfl_xor(v[r], j, WAVE);
+                    const double p = xor_lanes_f64(v[r], j);
                     const bool up = (((lane + WAVE * r) & k) == 0);
                     const bool lower = (lane & j) == 0;
-                    v[r] = lower == up ? hw_min(p, v[r]) : hw_max(p, v[r]);
+                    const double mn = hw_min(p, v[r]), mx = hw_max(p, v[r]);
+                    v[r] = lower == up ? mn : mx;
                 }
             }
         }
     }
 }
 
-// 32-bit keys, R == 1: one wave sorts its 64 lane values ascending (21 stages, one
-// ds_bpermute each, min/max instead of 64-bit compares and selects).
+// 32-bit keys, R == 1: one wave sorts its 64 lane values ascending (21 stages, one DPP /
+// permlane exchange each, min/max instead of 64-bit compares and selects).
 template <int R>
 __device__ __forceinline__ void wave_sort32(uint32_t (&v)[R]) {
     static_assert(R == 1, "wave_sort32: one register");
@@ -216,7 +219,7 @@ __device__ __forceinline__ void wave_sort32(uint32_t (&v)[R]) {
     for (int k = 2; k <= WAVE; k <<= 1) {
 #pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t p = (uint32_t)__shfl_xor((int)v[0], j, WAVE);
+            const uint32_t p = xor_lanes_u32(v[0], j);
             const bool up = (lane & k) == 0;
             const bool lower = (lane & j) == 0;
             const uint32_t mn = p < v[0] ? p : v[0], mx = p < v[0] ? v[0] : p;
@@ -540,188 +543,238 @@ __device__ __forceinline__ void pick_tail(const double* L, int c, int ra, int rb
     vb = rb < c ? at(rb) : tau;
 }
 
+// Issue the loads of unit u into xv (no value is used here: clamped 32-bit byte offsets,
+// masking happens at use, so the loads stay in flight while the caller keeps working).
+template <int VPL>
+__device__ __forceinline__ int load_unit(const SelArgs& a, int64_t u, double (&xv)[VPL]) {
+    typedef const __attribute__((address_space(1))) char* gptr;   // global_load, SGPR base
+    const int lane = lane_id();
+    const int s = (int)(u % a.nseg), c = (int)(u / a.nseg);
+    const int64_t r0 = a.seg_off[s];
+    const int L = (int)(a.seg_off[s + 1] - r0);
+    const gptr src = (gptr)(a.cols + (int64_t)c * a.col_stride + r0);
+    const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
+    // opaque lane offset: otherwise the loop-invariant per-row offsets are hoisted out of
+    // the unit loop and held in VGPRs for its whole length
+    uint32_t lb = (uint32_t)lane * 8u;
+    asm volatile("" : "+v"(lb));
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+        const uint32_t off = lb + (uint32_t)(v * WAVE * 8);
+        xv[v] = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
+    }
+    return L;
+}
+
+// Persistent waves, software-pipelined over units u = gw, gw + nwaves, ...: the loads of the
+// next unit are issued as soon as this unit's candidates are compacted into LDS, so they
+// overlap the candidate sorts, the lerp and the stores (without the moments pass, which
+// needs the values; then they are issued after it).
 template <int VPL>
 __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
     __shared__ double cbuf[SNW][2][WCAP];   // per wave: lower / upper tail candidates
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
-    const int64_t u = (int64_t)blockIdx.x * SNW + w;
-    if (u >= (int64_t)a.nseg * a.ncols) return;   // wave-uniform; no block barriers below
-    const int s = (int)(u % a.nseg), c = (int)(u / a.nseg);
-    const int64_t r0 = a.seg_off[s];
-    const int L = (int)(a.seg_off[s + 1] - r0);
-    typedef const __attribute__((address_space(1))) char* gptr;   // global_load, SGPR base
-    const gptr src = (gptr)(a.cols + (int64_t)c * a.col_stride + r0);
-    const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
-    // All loads are issued before any value is used (clamped 32-bit byte offsets, no
-    // masking here: masking at the load would make each load wait for its data).
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
+    const int64_t nwt = (int64_t)gridDim.x * SNW;
+    int64_t u = (int64_t)blockIdx.x * SNW + w;
+    if (u >= nunits) return;   // wave-uniform; no block barriers below
+    const bool early = a.mean == nullptr;   // prefetch right after compaction
     double xv[VPL];
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-        const uint32_t off = (uint32_t)(lane + v * WAVE) * 8u;
-        xv[v] = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
-    }
+    int L = load_unit<VPL>(a, u, xv);
     __builtin_amdgcn_sched_barrier(0);
-    // count / min / max with 4 independent accumulators each (the chains would otherwise
-    // serialize on the f64 latency)
-    int cnt4[4] = {0, 0, 0, 0};
-    double mn4[4] = {NAN, NAN, NAN, NAN}, mx4[4] = {NAN, NAN, NAN, NAN};
-    const int vfull = L / WAVE;   // rows v < vfull lie inside the segment (wave-uniform)
+    double* Ll = cbuf[w][0];
+    double* Lh = cbuf[w][1];
+    while (true) {
+        const int64_t un = u + nwt;
+        const bool more = un < nunits;
+        int Ln = 0;
+        // count / min / max with 4 independent accumulators each (the chains would otherwise
+        // serialize on the f64 latency)
+        int cnt4[4] = {0, 0, 0, 0};
+        double mn4[4] = {NAN, NAN, NAN, NAN}, mx4[4] = {NAN, NAN, NAN, NAN};
+        const int vfull = L / WAVE;   // rows v < vfull lie inside the segment (wave-uniform)
+        int lo_ = lane;
+        asm volatile("" : "+v"(lo_));   // keep lane + v * WAVE from being hoisted (see load_unit)
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-        if (v >= vfull && lane + v * WAVE >= L) xv[v] = NAN;   // past the segment end
-        cnt4[v & 3] += isnan(xv[v]) ? 0 : 1;
-        mn4[v & 3] = hw_min(mn4[v & 3], xv[v]);   // NaN-ignoring, no canonicalized copy of xv
-        mx4[v & 3] = hw_max(mx4[v & 3], xv[v]);
-    }
-    const double mn = hw_min(hw_min(mn4[0], mn4[1]), hw_min(mn4[2], mn4[3]));
-    const double mx = hw_max(hw_max(mx4[0], mx4[1]), hw_max(mx4[2], mx4[3]));
-    const int n = __builtin_amdgcn_readfirstlane(wave_sum((cnt4[0] + cnt4[1]) + (cnt4[2] + cnt4[3])));
-    double lo = NAN, hi = NAN;
-    if (n >= a.min_count && n > 0) {
-        int i0, j0, i1, j1;
-        double g0, g1;
-        qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
-        qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
-        const int ci = n - 1 - j1, cj = n - 1 - i1;   // upper ranks in complemented order
-        bool ok = j0 < WAVE && cj < WAVE;
-        double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-        if (ok) {
-            // tau from the high 32 bits of the keys (half the cost of a 64-bit sort): the
-            // j0-th smallest high word T bounds j0+1 lane minima by key (T << 32 | ~0), so
-            // that key is as valid a tau as an exact lane minimum (and s[j0] is a candidate
-            // whenever tau is not itself a data value)
-            const uint32_t ha = isnan(mn) ? 0xFFFFFFFFu : (uint32_t)(dkey(mn) >> 32);
-            const uint32_t hb = isnan(mx) ? 0xFFFFFFFFu : (uint32_t)(~dkey(mx) >> 32);
-            uint32_t ta[1] = {ha};
-            uint32_t tb[1] = {hb};
-            wave_sort32<1>(ta);
-            wave_sort32<1>(tb);
-            const uint32_t Ta = (uint32_t)__builtin_amdgcn_readlane((int)ta[0], j0);
-            const uint32_t Tb = (uint32_t)__builtin_amdgcn_readlane((int)tb[0], cj);
-            ok = Ta != 0xFFFFFFFFu && Tb != 0xFFFFFFFFu;
+        for (int v = 0; v < VPL; ++v) {
+            if (v >= vfull && lo_ + v * WAVE >= L) xv[v] = NAN;   // past the segment end
+            cnt4[v & 3] += isnan(xv[v]) ? 0 : 1;
+            mn4[v & 3] = hw_min(mn4[v & 3], xv[v]);   // NaN-ignoring, no canonicalized copy of xv
+            mx4[v & 3] = hw_max(mx4[v & 3], xv[v]);
+        }
+        const double mn = hw_min(hw_min(mn4[0], mn4[1]), hw_min(mn4[2], mn4[3]));
+        const double mx = hw_max(hw_max(mx4[0], mx4[1]), hw_max(mx4[2], mx4[3]));
+        int cn = (cnt4[0] + cnt4[1]) + (cnt4[2] + cnt4[3]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cn += (int)xor_lanes_u32((uint32_t)cn, o);
+        const int n = __builtin_amdgcn_readfirstlane(cn);
+        double lo = NAN, hi = NAN;
+        bool ok = true;
+        const bool apply = n >= a.min_count && n > 0;
+        int i0 = 0, j0 = 0, i1 = 0, j1 = 0, clo = 0, chi = 0;
+        double g0 = 0.0, g1 = 0.0, tlo = NAN, thi = NAN;
+        if (apply) {
+            qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
+            qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
+            const int cj = n - 1 - i1;   // upper rank in complemented order
+            ok = j0 < WAVE && cj < WAVE;
             if (ok) {
-                // tau = the largest lane minimum whose high word is Ta: at least j0+1 lane
-                // minima are <= it, and it is a data value, so ties at tau (e.g. many exact
-                // zeros) stay out of the candidates instead of overflowing them
-                double tlo = ha == Ta ? mn : NAN, thi = hb == Tb ? mx : NAN;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    tlo = hw_max(tlo, __shfl_xor(tlo, o, WAVE));
-                    thi = hw_min(thi, __shfl_xor(thi, o, WAVE));
-                }
-                double* Ll = cbuf[w][0];
-                double* Lh = cbuf[w][1];
-                int clo = 0, chi = 0;   // wave-uniform running counts; overflow is checked once
-#pragma unroll
-                for (int v = 0; v < VPL; ++v) {
-                    const bool bl = xv[v] < tlo, bh = xv[v] > thi;
-                    const uint64_t ml = __ballot(bl), mh = __ballot(bh);
-                    if (ml) {
-                        if (bl) Ll[(clo + mask_rank(ml)) & (WCAP - 1)] = xv[v];
-                        clo += (int)__popcll(ml);
-                    }
-                    if (mh) {
-                        if (bh) Lh[(chi + mask_rank(mh)) & (WCAP - 1)] = -xv[v];   // ascending
-                        chi += (int)__popcll(mh);
-                    }
-                }
-                ok = clo <= WCAP && chi <= WCAP;
+                // tau from the high 32 bits of the keys (half the cost of a 64-bit sort): the
+                // j0-th smallest high word T bounds j0+1 lane minima by key (T << 32 | ~0)
+                const uint32_t ha = isnan(mn) ? 0xFFFFFFFFu : (uint32_t)(dkey(mn) >> 32);
+                const uint32_t hb = isnan(mx) ? 0xFFFFFFFFu : (uint32_t)(~dkey(mx) >> 32);
+                uint32_t ta[1] = {ha};
+                uint32_t tb[1] = {hb};
+                wave_sort32<1>(ta);
+                wave_sort32<1>(tb);
+                const uint32_t Ta = (uint32_t)__builtin_amdgcn_readlane((int)ta[0], j0);
+                const uint32_t Tb = (uint32_t)__builtin_amdgcn_readlane((int)tb[0], cj);
+                ok = Ta != 0xFFFFFFFFu && Tb != 0xFFFFFFFFu;
                 if (ok) {
-                    // LDS executes one wave's DS instructions in order; only the compiler's
-                    // reordering must be fenced
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    // the candidates are never NaN: sort them as doubles (hardware min/max;
-                    // equal values, +0 / -0 included, are interchangeable for the result)
-                    if (clo <= 2 * WAVE && chi <= 2 * WAVE) {
-                        pick_tail<2>(Ll, clo, i0, j0, tlo, v0, v1);
-                        pick_tail<2>(Lh, chi, ci, cj, -thi, v3, v2);
-                    } else {   // heavy tails: rare, 256 candidates
-                        pick_tail<4>(Ll, clo, i0, j0, tlo, v0, v1);
-                        pick_tail<4>(Lh, chi, ci, cj, -thi, v3, v2);
+                    // tau = the largest lane minimum whose high word is Ta: at least j0+1 lane
+                    // minima are <= it, and it is a data value, so ties at tau (e.g. many
+                    // exact zeros) stay out of the candidates instead of overflowing them
+                    tlo = ha == Ta ? mn : NAN;
+                    thi = hb == Tb ? mx : NAN;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) {   // whole wave active: DPP / permlane
+                        tlo = hw_max(tlo, xor_lanes_f64(tlo, o));
+                        thi = hw_min(thi, xor_lanes_f64(thi, o));
                     }
-                    v2 = -v2;   // upper tail: candidates were stored negated (ascending)
-                    v3 = -v3;
+                    // wave-uniform running counts; overflow is checked once
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v) {
+                        const bool bl = xv[v] < tlo, bh = xv[v] > thi;
+                        const uint64_t ml = __ballot(bl), mh = __ballot(bh);
+                        if (ml) {
+                            if (bl) Ll[(clo + mask_rank(ml)) & (WCAP - 1)] = xv[v];
+                            clo += (int)__popcll(ml);
+                        }
+                        if (mh) {
+                            if (bh) Lh[(chi + mask_rank(mh)) & (WCAP - 1)] = -xv[v];   // ascending
+                            chi += (int)__popcll(mh);
+                        }
+                    }
+                    ok = clo <= WCAP && chi <= WCAP;
                 }
             }
+        }
+        if (early && more) Ln = load_unit<VPL>(a, un, xv);   // xv is free from here on
+        if (apply && ok) {
+            double v0, v1, v2, v3;
+            const int ci = n - 1 - j1, cj = n - 1 - i1;
+            // LDS executes one wave's DS instructions in order; only the compiler's
+            // reordering must be fenced
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the candidates are never NaN: sort them as doubles (hardware min/max; equal
+            // values, +0 / -0 included, are interchangeable for the result)
+            if (clo <= 2 * WAVE && chi <= 2 * WAVE) {
+                pick_tail<2>(Ll, clo, i0, j0, tlo, v0, v1);
+                pick_tail<2>(Lh, chi, ci, cj, -thi, v3, v2);
+            } else {   // heavy tails: rare, 256 candidates
+                pick_tail<4>(Ll, clo, i0, j0, tlo, v0, v1);
+                pick_tail<4>(Lh, chi, ci, cj, -thi, v3, v2);
+            }
+            lo = qlerp(v0, v1, g0, a.lerp_mode);
+            hi = qlerp(-v2, -v3, g1, a.lerp_mode);   // upper tail was stored negated
+            // keep the LDS lists intact until every lane has read them (next unit rewrites)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         if (!ok) {
             if (lane == 0 && a.nvalid) a.nvalid[u] = -1;   // redone by the fallback pass
-            return;
-        }
-        lo = qlerp(v0, v1, g0, a.lerp_mode);
-        hi = qlerp(v2, v3, g1, a.lerp_mode);
-    }
-    if (a.center != nullptr) {
-        // Gram pivot: the midpoint of the cuts, else of the values' range, else 0
-        double cen = 0.5 * (lo + hi);
-        if (!isfinite(cen)) {
-            double m1 = isfinite(mn) ? mn : NAN, m2 = isfinite(mx) ? mx : NAN;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                m1 = hw_min(m1, __shfl_xor(m1, o, WAVE));
-                m2 = hw_max(m2, __shfl_xor(m2, o, WAVE));
-            }
-            cen = 0.5 * (m1 + m2);
-            if (!isfinite(cen)) cen = 0.0;
-        }
-        if (lane == 0) a.center[u] = cen;
-    }
-    if (a.mean != nullptr) {
-        // moments of the clipped values about a pivot inside the data (see select_unit_wg)
-        double p = isfinite(lo) ? lo : (isfinite(hi) ? hi : 0.0);
-        if (!isfinite(lo) && !isfinite(hi)) {
-            double m2 = isfinite(mn) ? mn : NAN;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m2 = fmin(m2, __shfl_xor(m2, o, WAVE));
-            p = isfinite(m2) ? m2 : 0.0;
-        }
-        double s1 = 0.0, s2 = 0.0;
-        if (isfinite(lo) && !isnan(hi)) {
-            // p == lo: hardware max/min send a NaN (absent) value to lo, so it adds d == 0
-            // exactly; the same d as the general loop for every present value
-#pragma unroll
-            for (int v = 0; v < VPL; ++v) {
-                const double d = hw_min(hw_max(xv[v], lo), hi) - lo;
-                s1 += d;
-                s2 = fma(d, d, s2);
-            }
         } else {
+            if (a.center != nullptr) {
+                // Gram pivot: the midpoint of the cuts, else of the values' range, else 0
+                double cen = 0.5 * (lo + hi);
+                if (!isfinite(cen)) {
+                    double m1 = isfinite(mn) ? mn : NAN, m2 = isfinite(mx) ? mx : NAN;
 #pragma unroll
-            for (int v = 0; v < VPL; ++v) {
-                double x = xv[v];
-                if (x < lo) x = lo;
-                if (x > hi) x = hi;
-                const double d = isnan(x) ? 0.0 : x - p;
-                s1 += d;
-                s2 = fma(d, d, s2);
+                    for (int o = 32; o > 0; o >>= 1) {
+                        m1 = hw_min(m1, xor_lanes_f64(m1, o));
+                        m2 = hw_max(m2, xor_lanes_f64(m2, o));
+                    }
+                    cen = 0.5 * (m1 + m2);
+                    if (!isfinite(cen)) cen = 0.0;
+                }
+                if (lane == 0) a.center[u] = cen;
+            }
+            if (!early) {
+                // moments of the clipped values about a pivot inside the data (see
+                // select_unit_wg)
+                double p = isfinite(lo) ? lo : (isfinite(hi) ? hi : 0.0);
+                if (!isfinite(lo) && !isfinite(hi)) {
+                    double m2 = isfinite(mn) ? mn : NAN;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) m2 = fmin(m2, __shfl_xor(m2, o, WAVE));
+                    p = isfinite(m2) ? m2 : 0.0;
+                }
+                double s1 = 0.0, s2 = 0.0;
+                if (isfinite(lo) && !isnan(hi)) {
+                    // p == lo: hardware max/min send a NaN (absent) value to lo, so it adds
+                    // d == 0 exactly; the same d as the general loop for every present value
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v) {
+                        const double d = hw_min(hw_max(xv[v], lo), hi) - lo;
+                        s1 += d;
+                        s2 = fma(d, d, s2);
+                    }
+                } else {
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v) {
+                        double x = xv[v];
+                        if (x < lo) x = lo;
+                        if (x > hi) x = hi;
+                        const double d = isnan(x) ? 0.0 : x - p;
+                        s1 += d;
+                        s2 = fma(d, d, s2);
+                    }
+                }
+                s1 = wave_sum(s1);
+                s2 = wave_sum(s2);
+                if (lane == 0) {
+                    a.mean[u] = n > 0 ? p + s1 / (double)n : NAN;
+                    if (a.sd) {
+                        double var = n > 1 ? (s2 - s1 * (s1 / (double)n)) / (double)(n - 1) : NAN;
+                        if (var < 0.0) var = 0.0;
+                        a.sd[u] = n > 1 ? sqrt(var) : NAN;
+                    }
+                }
+            }
+            if (lane == 0) {
+                a.lo[u] = lo;
+                a.hi[u] = hi;
+                if (a.nvalid) a.nvalid[u] = n;
             }
         }
-        s1 = wave_sum(s1);
-        s2 = wave_sum(s2);
-        if (lane == 0) {
-            a.mean[u] = n > 0 ? p + s1 / (double)n : NAN;
-            if (a.sd) {
-                double var = n > 1 ? (s2 - s1 * (s1 / (double)n)) / (double)(n - 1) : NAN;
-                if (var < 0.0) var = 0.0;
-                a.sd[u] = n > 1 ? sqrt(var) : NAN;
-            }
-        }
+        if (!more) break;
+        if (!early) Ln = load_unit<VPL>(a, un, xv);
+        u = un;
+        L = Ln;
     }
-    if (lane == 0) {
-        a.lo[u] = lo;
-        a.hi[u] = hi;
-        if (a.nvalid) a.nvalid[u] = n;
-    }
+}
+
+int select_wave_grid(int64_t nunits) {
+    static int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int64_t need = (nunits + SNW - 1) / SNW;
+    const int64_t cap = (int64_t)ncu * 2;   // two resident workgroups per CU
+    return (int)(need < cap ? need : cap);
 }
 
 template <int VPL>
 void launch_select_wave(const SelArgs& a, hipStream_t st) {
     const int64_t nunits = (int64_t)a.nseg * a.ncols;
-    hipLaunchKernelGGL(select_wave_kernel<VPL>, dim3((unsigned)((nunits + SNW - 1) / SNW)), dim3(ST), 0,
-                       st, a);
+    hipLaunchKernelGGL(select_wave_kernel<VPL>, dim3((unsigned)select_wave_grid(nunits)), dim3(ST), 0, st, a);
 }
 
 }  // namespace
