@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "fm_hip.h"
 
 namespace fm {
@@ -46,6 +48,15 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
     return ((uint64_t)hi << 32) | lo;
+}
+
+// compile-time loop: f(std::integral_constant<int, i>) for i in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
 }
 
 // Value of lane (this lane ^ J), without LDS: DPP quad_perm (1, 2), two bank-masked DPP

@@ -174,58 +174,117 @@ __device__ __forceinline__ void wave_sort(uint64_t (&v)[R]) {
     }
 }
 
-// Non-NaN doubles (element e = lane + 64 r in register r): bitonic sort ascending with the
-// hardware min / max (no 64-bit integer compares and selects).  Cross-lane stages exchange
-// through DPP / permlane swaps (no LDS round trip); both min and max are computed and the
-// lane's role selects one (inline asm is convergent: a conditional one becomes a branch).
-template <int R>
-__device__ __forceinline__ void wave_sort_f64(double (&v)[R]) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int k = 2; k <= WAVE * R; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= WAVE) {
-                const int rj = j / WAVE;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (r & rj) continue;
-                    const bool up = (((lane + WAVE * r) & k) == 0);
-                    const double mn = hw_min(v[r], v[r | rj]), mx = hw_max(v[r], v[r | rj]);
-                    v[r] = up ? mn : mx;
-                    v[r | rj] = up ? mx : mn;
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const double p = xor_lanes_f64(v[r], j);
-                    const bool up = (((lane + WAVE * r) & k) == 0);
-                    const bool lower = (lane & j) == 0;
-                    const double mn = hw_min(p, v[r]), mx = hw_max(p, v[r]);
-                    v[r] = lower == up ? mn : mx;
-                }
-            }
+// Bitonic stage (k, j) for register r (element e = lane + 64 r): lane l keeps the minimum
+// iff ((l & j) == 0) == ((e & k) == 0).  As a compile-time 64-bit lane mask the role costs
+// one s_mov_b64 instead of per-stage lane arithmetic.
+template <int K, int J, int Rr>
+__host__ __device__ constexpr uint64_t bitonic_min_mask() {
+    uint64_t m = 0;
+    for (int l = 0; l < WAVE; ++l)
+        if (((l & J) == 0) == (((l + WAVE * Rr) & K) == 0)) m |= 1ull << l;
+    return m;
+}
+// mask bit set ? if1 : if0 (v_cndmask with an SGPR-pair condition)
+__device__ __forceinline__ uint32_t cnd_u32(uint64_t m, uint32_t if0, uint32_t if1) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
+    return r;
+}
+__device__ __forceinline__ double cnd_f64(uint64_t m, double if0, double if1) {
+    const uint64_t a = (uint64_t)__double_as_longlong(if0), b = (uint64_t)__double_as_longlong(if1);
+    const uint32_t lo = cnd_u32(m, (uint32_t)a, (uint32_t)b);
+    const uint32_t hi = cnd_u32(m, (uint32_t)(a >> 32), (uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// {own, partner at lane ^ J} as an unordered pair: for J in {16, 32} a permlane swap of a
+// register with itself leaves each lane holding both; for J < 16 (own, DPP partner)
+template <int J>
+__device__ __forceinline__ void xor_pair_f64(double x, double& p0, double& p1) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    if constexpr (J >= 16) {
+        const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+        uint32_t l0, l1, h0, h1;
+        if constexpr (J == 16) {
+            const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+            const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+            l0 = rl[0], l1 = rl[1], h0 = rh[0], h1 = rh[1];
+        } else {
+            const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+            const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+            l0 = rl[0], l1 = rl[1], h0 = rh[0], h1 = rh[1];
         }
+        p0 = __longlong_as_double((long long)(((uint64_t)h0 << 32) | l0));
+        p1 = __longlong_as_double((long long)(((uint64_t)h1 << 32) | l1));
+    } else {
+        p0 = x;
+        p1 = __longlong_as_double((long long)(((uint64_t)xor_lanes<J>((uint32_t)(b >> 32)) << 32) |
+                                              xor_lanes<J>((uint32_t)b)));
+    }
+}
+template <int J>
+__device__ __forceinline__ void xor_pair_u32(uint32_t x, uint32_t& p0, uint32_t& p1) {
+    if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        p0 = r[0], p1 = r[1];
+    } else if constexpr (J == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        p0 = r[0], p1 = r[1];
+    } else {
+        p0 = x, p1 = xor_lanes<J>(x);
     }
 }
 
+template <int R, int K, int J>
+__device__ __forceinline__ void bitonic_f64_stages(double (&v)[R]) {
+    if constexpr (J >= WAVE) {   // register-local: the role depends on r only
+        constexpr int rj = J / WAVE;
+        static_for<0, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            if constexpr ((r & rj) == 0) {
+                constexpr bool up = ((WAVE * r) & K) == 0;
+                const double mn = hw_min(v[r], v[r | rj]), mx = hw_max(v[r], v[r | rj]);
+                v[r] = up ? mn : mx;
+                v[r | rj] = up ? mx : mn;
+            }
+        });
+    } else {
+        static_for<0, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            double p0, p1;
+            xor_pair_f64<J>(v[r], p0, p1);
+            const double mn = hw_min(p0, p1), mx = hw_max(p0, p1);
+            v[r] = cnd_f64(bitonic_min_mask<K, J, r>(), mx, mn);
+        });
+    }
+    if constexpr (J > 1) bitonic_f64_stages<R, K, J / 2>(v);
+}
+
+// Non-NaN doubles (element e = lane + 64 r in register r): bitonic sort ascending with the
+// hardware min / max (no 64-bit integer compares and selects).  Cross-lane stages exchange
+// through DPP / permlane swaps (no LDS round trip); min and max are both computed and a
+// constant lane mask picks one (inline asm is convergent: a conditional one would branch).
+template <int R, int K = 2>
+__device__ __forceinline__ void wave_sort_f64(double (&v)[R]) {
+    bitonic_f64_stages<R, K, K / 2>(v);
+    if constexpr (K < WAVE * R) wave_sort_f64<R, K * 2>(v);
+}
+
+template <int K, int J>
+__device__ __forceinline__ void bitonic_u32_stages(uint32_t& v) {
+    uint32_t p0, p1;
+    xor_pair_u32<J>(v, p0, p1);
+    const uint32_t mn = p0 < p1 ? p0 : p1, mx = p0 < p1 ? p1 : p0;
+    v = cnd_u32(bitonic_min_mask<K, J, 0>(), mx, mn);
+    if constexpr (J > 1) bitonic_u32_stages<K, J / 2>(v);
+}
+
 // 32-bit keys, R == 1: one wave sorts its 64 lane values ascending (21 stages, one DPP /
-// permlane exchange each, min/max instead of 64-bit compares and selects).
-template <int R>
+// permlane exchange each).
+template <int R, int K = 2>
 __device__ __forceinline__ void wave_sort32(uint32_t (&v)[R]) {
     static_assert(R == 1, "wave_sort32: one register");
-    const int lane = lane_id();
-#pragma unroll
-    for (int k = 2; k <= WAVE; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t p = xor_lanes_u32(v[0], j);
-            const bool up = (lane & k) == 0;
-            const bool lower = (lane & j) == 0;
-            const uint32_t mn = p < v[0] ? p : v[0], mx = p < v[0] ? v[0] : p;
-            v[0] = lower == up ? mn : mx;
-        }
-    }
+    bitonic_u32_stages<K, K / 2>(v[0]);
+    if constexpr (K < WAVE) wave_sort32<R, K * 2>(v);
 }
 
 // Sort buf[0..c) (c <= 64*R) in place with one wave; entries c..64R-1 become SENT.
@@ -589,9 +648,10 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
         const int64_t un = u + nwt;
         const bool more = un < nunits;
         int Ln = 0;
-        // count / min / max with 4 independent accumulators each (the chains would otherwise
-        // serialize on the f64 latency)
-        int cnt4[4] = {0, 0, 0, 0};
+        // min / max with 4 independent accumulators each (the chains would otherwise serialize
+        // on the f64 latency)
+        // (the count is scalar: ballot + popcount per row, no VALU)
+        int n = 0;
         double mn4[4] = {NAN, NAN, NAN, NAN}, mx4[4] = {NAN, NAN, NAN, NAN};
         const int vfull = L / WAVE;   // rows v < vfull lie inside the segment (wave-uniform)
         int lo_ = lane;
@@ -599,16 +659,13 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
 #pragma unroll
         for (int v = 0; v < VPL; ++v) {
             if (v >= vfull && lo_ + v * WAVE >= L) xv[v] = NAN;   // past the segment end
-            cnt4[v & 3] += isnan(xv[v]) ? 0 : 1;
+            n += (int)__popcll(__ballot(!isnan(xv[v])));
             mn4[v & 3] = hw_min(mn4[v & 3], xv[v]);   // NaN-ignoring, no canonicalized copy of xv
             mx4[v & 3] = hw_max(mx4[v & 3], xv[v]);
         }
         const double mn = hw_min(hw_min(mn4[0], mn4[1]), hw_min(mn4[2], mn4[3]));
         const double mx = hw_max(hw_max(mx4[0], mx4[1]), hw_max(mx4[2], mx4[3]));
-        int cn = (cnt4[0] + cnt4[1]) + (cnt4[2] + cnt4[3]);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) cn += (int)xor_lanes_u32((uint32_t)cn, o);
-        const int n = __builtin_amdgcn_readfirstlane(cn);
+        n = __builtin_amdgcn_readfirstlane(n);
         double lo = NAN, hi = NAN;
         bool ok = true;
         const bool apply = n >= a.min_count && n > 0;

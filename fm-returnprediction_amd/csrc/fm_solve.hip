@@ -315,13 +315,6 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
 // row_newbcast moves (VALU modifiers: no LDS round trip, no readlane hazards) and four
 // factorizations run in the time of one.  Rank-deficient problems (rare) take the Jacobi
 // pseudo-inverse path one at a time.
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        static_for<B + 1, E>(f);
-    }
-}
 
 template <int L>
 __device__ __forceinline__ int rowbc_i(int v) {   // lane L of this lane's 16-lane row
