@@ -278,20 +278,19 @@ def test_mid_panel_golden(R):
 
 
 # ---------------------------------------------------------------- full pipeline vs oracle
-@pytest.mark.parametrize("fused", [True, False], ids=["ts_fused", "ts_per_stage"])
-def test_pipeline_vs_oracle(E, fused, monkeypatch):
+def _pipeline_vs_oracle(E, T, N, seed, model_cols=None, fig1=True):
     from fmcore import lewellen as LW, synth
-    if not fused:   # the per-stage kernels that serve series too long for LDS staging
-        monkeypatch.setattr(E, "ts_fused_fits", lambda *a, **k: False)
-    T, N = 150, 400
-    a = synth.synth_arrays(T, N, 99, nan_rate=0.03, present_rate=0.9)
-    cols = list(dict.fromkeys(["retx"] + [c for xs in LW.table2_models().values() for c in xs] + LW.FIG1_VARS))
+    model_cols = model_cols or LW.table2_models()
+    a = synth.synth_arrays(T, N, seed, nan_rate=0.03, present_rate=0.9)
+    cols = list(dict.fromkeys(["retx"] + [c for xs in model_cols.values() for c in xs] +
+                              (LW.FIG1_VARS if fig1 else [])))
     panel = E.panel_from_arrays([a[c] for c in cols], cols, a["month"], me=a["me"], nyse=a["nyse"])
-    out = LW.run_pipeline(panel, LW.PipelineConfig(), model_cols=LW.table2_models())
+    out = LW.run_pipeline(panel, LW.PipelineConfig(fig1=fig1), model_cols=model_cols)
     seg_off = panel.seg_off_h
     srt = {c: a[c][panel.order] for c in cols}
-    models = {name: ("retx", xs, (0, 1, 2)) for name, xs in LW.table2_models().items()}
-    models["Figure 1"] = ("retx", LW.FIG1_VARS, (0, 2))
+    models = {name: ("retx", xs, (0, 1, 2)) for name, xs in model_cols.items()}
+    if fig1:
+        models["Figure 1"] = ("retx", LW.FIG1_VARS, (0, 2))
     ref = O.pipeline_arrays(srt, seg_off, a["me"][panel.order], a["nyse"][panel.order].astype(bool), models,
                             None)
     res = out.res
@@ -304,6 +303,7 @@ def test_pipeline_vs_oracle(E, fused, monkeypatch):
     pst = out.pred_status.cpu().numpy()
     pmean = out.pred_summary.mean.cpu().numpy()
     ptst = out.pred_summary.tstat.cpu().numpy()
+    assert len(res.problems) == sum(len(m[2]) for m in models.values())
     for k, p in enumerate(res.problems):
         name = out.model_names[p.model]
         r = ref[(name, p.level)]
@@ -323,6 +323,28 @@ def test_pipeline_vs_oracle(E, fused, monkeypatch):
         assert_series_close(pred[k, pf, 1], r["pred_R2"], f"{name} pred R2")
         assert scalar_close(pmean[k, 0], r["pred_summary"][0], RTOL, 1e-12)
         assert scalar_close(ptst[k, 0], r["pred_summary"][1], RTOL, 1e-12)
+
+
+@pytest.mark.parametrize("fused", [True, False], ids=["ts_fused", "ts_per_stage"])
+def test_pipeline_vs_oracle(E, fused, monkeypatch):
+    """C3/C4 shape (all Table-2 models x 3 universes + Figure 1), 150 months x 400 firms."""
+    if not fused:   # the per-stage kernels that serve series too long for LDS staging
+        monkeypatch.setattr(E, "ts_fused_fits", lambda *a, **k: False)
+    _pipeline_vs_oracle(E, 150, 400, 99)
+
+
+def test_pipeline_c5_month_width(E):
+    """C5 month width: 20,000 firms per month (> the wave select's 6,144-row register
+    budget, so the cuts take the workgroup select path), 12 months."""
+    _pipeline_vs_oracle(E, 12, 20000, 7)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_pipeline_single_model_configs(E, cfg):
+    """C1 (Model 1, K=3) and C2 (Model 2, K=7) alone, 3 universes, no Figure 1."""
+    from fmcore import lewellen as LW
+    name = {"C1": "Model 1: Three Predictors", "C2": "Model 2: Seven Predictors"}[cfg]
+    _pipeline_vs_oracle(E, 80, 600, 11, model_cols={name: LW.table2_models()[name]}, fig1=False)
 
 
 def test_table1_golden(CL):

@@ -1,5 +1,5 @@
 """Time fm_gram alone on the bench panel for several chunk sizes (HIP events on the launch
-stream).  python tools/gram_sweep.py [chunk_rows ...]"""
+stream, engine.time_launch).  python tools/gram_sweep.py [chunk_rows ...]"""
 import os
 import sys
 
@@ -23,12 +23,10 @@ def main():
         for _ in range(3):
             LW.local_stage(panel, cfg, LW.table2_models())
         torch.cuda.synchronize()
-        with E.KernelTimer() as t:
-            for _ in range(10):
-                LW.local_stage(panel, cfg, LW.table2_models())
+        # device time of the latest launch re-issued back to back (no host gaps)
         print(f"chunk_rows={ch} nchunks={E._chunk_plan(panel).nchunks} "
-              f"gram_ms={t.avg_ms('fm_gram'):.4f} solve_ms={t.avg_ms('fm_solve'):.4f} "
-              f"select_ms={t.avg_ms('fm_select_cuts'):.4f}", flush=True)
+              f"gram_ms={E.time_launch('fm_gram', 50):.4f} solve_ms={E.time_launch('fm_solve', 50):.4f}",
+              flush=True)
 
 
 if __name__ == "__main__":
