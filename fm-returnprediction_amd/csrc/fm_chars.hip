@@ -1,0 +1,273 @@
+// Firm-axis characteristic construction: the per-firm lags,
+// rolling windows and log / ratio arithmetic that get_factors runs before winsorize
+// (reference src/calc_Lewellen_2014.py:531-575), as two HBM-streaming kernels over a
+// FIRM-major panel (rows grouped by permno, each group in frame order).
+//
+//   firm_chars_kernel  <- calc_log_size .. calc_sales_price (:137-341): one workgroup per
+//                         256-row tile, one row per thread.  The 36-row halo of firm ids and
+//                         the return-derived window inputs (1 + retx, log(1 + retx), dvc)
+//                         are staged in LDS once per tile; lag-k reads of the other fields
+//                         are coalesced global loads that hit L2 (the previous tile's rows).
+//                         Because groups are contiguous, "row i-k belongs to row i's firm" is
+//                         one compare: ids[i-k] == ids[i].
+//   rolling_std_kernel <- calc_std_12's 252-day rolling std (:448-456): each thread owns 8
+//                         consecutive rows; the first window is summed directly (two-pass
+//                         from LDS), the next 7 slide by Welford remove/add.  pandas slides
+//                         one Welford/Kahan state along the whole group; both agree to
+//                         rounding (tests: 1e-9 series-RMS tolerance).
+#include <math.h>
+
+#include "fm_common.h"
+
+namespace fm {
+namespace {
+
+constexpr int CT = 256;   // rows per firm_chars tile (= threads)
+constexpr int CH = 36;    // longest lag (calc_log_issues_36 / calc_log_return_13_36)
+
+__device__ __forceinline__ double nan_if_inf(double x) { return isinf(x) ? (double)NAN : x; }
+
+__global__ __launch_bounds__(CT) void firm_chars_kernel(fm_chars_args a, int need_ret, int need_dvc) {
+    __shared__ int64_t sid[CT + CH];
+    __shared__ double opr[CT + CH];   // 1 + retx, +-inf -> NaN (rolling input, :178-186)
+    __shared__ double lr[CT + CH];    // log(1 + retx), +-inf -> NaN (:298, :302-306)
+    __shared__ double dv[CT + CH];    // dvc, +-inf -> NaN (:273-278)
+    const int64_t n = a.n;
+    const int64_t b = (int64_t)blockIdx.x * CT;
+    const double* retx = a.field[FM_FIELD_RETX];
+    const double* dvc = a.field[FM_FIELD_DVC];
+    for (int j = threadIdx.x; j < CT + CH; j += CT) {
+        const int64_t r = b - CH + j;
+        const bool in = r >= 0 && r < n;
+        sid[j] = in ? a.ids[r] : 0;
+        if (need_ret) {
+            const double x = in ? retx[r] : (double)NAN;
+            const double o = 1.0 + x;
+            opr[j] = nan_if_inf(o);
+            lr[j] = nan_if_inf(log(o));
+        }
+        if (need_dvc) dv[j] = in ? nan_if_inf(dvc[r]) : (double)NAN;
+    }
+    __syncthreads();
+    const int64_t i = b + threadIdx.x;
+    if (i >= n) return;
+    const int li = threadIdx.x + CH;
+    const int64_t id = sid[li];
+    auto same = [&](int k) { return i - k >= 0 && sid[li - k] == id; };
+    // lag-k value of a field (NaN outside the firm); the load is clamped, not branched
+    auto lag = [&](int f, int k) {
+        const double* p = a.field[f];
+        const double v = p[i - k >= 0 ? i - k : 0];
+        return same(k) ? v : (double)NAN;
+    };
+    double* const* o = a.out;
+    const bool need_me1 = o[FM_CHAR_LOG_SIZE] || o[FM_CHAR_LOG_BM] || o[FM_CHAR_DEBT_PRICE] ||
+                          o[FM_CHAR_SALES_PRICE];
+    const double me1 = need_me1 ? lag(FM_FIELD_ME, 1) : 0.0;
+    if (o[FM_CHAR_LOG_SIZE]) o[FM_CHAR_LOG_SIZE][i] = log(me1);
+    if (o[FM_CHAR_LOG_BM]) o[FM_CHAR_LOG_BM][i] = log(lag(FM_FIELD_BE, 1)) - log(me1);
+    if (o[FM_CHAR_RETURN_12_2]) {
+        // rolling(11, min_periods=11).apply(np.prod) of the shift(2) column: rows t-12..t-2,
+        // oldest first; any NaN in the window -> NaN (the product propagates it)
+        double p = opr[li - 12];
+#pragma unroll
+        for (int k = 11; k >= 2; --k) p *= opr[li - k];
+        o[FM_CHAR_RETURN_12_2][i] = same(12) ? p - 1.0 : (double)NAN;
+    }
+    if (o[FM_CHAR_ACCRUALS_FINAL])
+        o[FM_CHAR_ACCRUALS_FINAL][i] = a.field[FM_FIELD_ACCRUALS][i] - a.field[FM_FIELD_DEPRECIATION][i];
+    if (o[FM_CHAR_ROA]) o[FM_CHAR_ROA][i] = a.field[FM_FIELD_EARNINGS][i] / a.field[FM_FIELD_ASSETS][i];
+    if (o[FM_CHAR_LOG_ASSETS_GROWTH])
+        o[FM_CHAR_LOG_ASSETS_GROWTH][i] = log(a.field[FM_FIELD_ASSETS][i] / lag(FM_FIELD_ASSETS, 12));
+    if (o[FM_CHAR_DY]) {
+        // rolling(12, min_periods=1).sum(): the observations among the firm's last 12 rows
+        double s = 0.0;
+        int cnt = 0;
+#pragma unroll
+        for (int k = 11; k >= 0; --k) {
+            const double v = dv[li - k];
+            const bool ok = same(k) && !isnan(v);
+            s += ok ? v : 0.0;
+            cnt += ok ? 1 : 0;
+        }
+        o[FM_CHAR_DY][i] = (cnt > 0 ? s : (double)NAN) / lag(FM_FIELD_PRC, 1);
+    }
+    if (o[FM_CHAR_LOG_RETURN_13_36]) {
+        // rolling(24, min_periods=24).sum() of the shift(13) column: all 24 rows t-36..t-13
+        double s = 0.0;
+#pragma unroll
+        for (int k = 36; k >= 13; --k) s += lr[li - k];
+        o[FM_CHAR_LOG_RETURN_13_36][i] = same(36) ? s : (double)NAN;
+    }
+    if (o[FM_CHAR_LOG_ISSUES_12] || o[FM_CHAR_LOG_ISSUES_36]) {
+        const double l1 = log(lag(FM_FIELD_SHROUT, 1));
+        if (o[FM_CHAR_LOG_ISSUES_12]) o[FM_CHAR_LOG_ISSUES_12][i] = l1 - log(lag(FM_FIELD_SHROUT, 12));
+        if (o[FM_CHAR_LOG_ISSUES_36]) o[FM_CHAR_LOG_ISSUES_36][i] = l1 - log(lag(FM_FIELD_SHROUT, 36));
+    }
+    if (o[FM_CHAR_DEBT_PRICE]) o[FM_CHAR_DEBT_PRICE][i] = a.field[FM_FIELD_TOTAL_DEBT][i] / me1;
+    if (o[FM_CHAR_SALES_PRICE]) o[FM_CHAR_SALES_PRICE][i] = a.field[FM_FIELD_SALES][i] / me1;
+}
+
+// ---- rolling std --------------------------------------------------------------------------
+constexpr int ST_T = 256;            // threads
+constexpr int ST_R = 8;              // consecutive rows per thread
+constexpr int ST_ROWS = ST_T * ST_R; // rows per tile
+
+// LDS slot of halo element e: one pad slot per 8 (lanes 8 rows apart hit distinct banks)
+__host__ __device__ __forceinline__ int spad(int e) { return e + (e >> 3); }
+
+__global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __restrict__ ids,
+                                                           const double* __restrict__ x, int64_t n,
+                                                           int W, int minp, double scale,
+                                                           double* __restrict__ out) {
+    extern __shared__ double sm[];
+    const int H = W - 1;
+    const int E = ST_ROWS + H;
+    double* xs = sm;
+    int64_t* is = (int64_t*)(sm + spad(E) + 1);
+    const int64_t b = (int64_t)blockIdx.x * ST_ROWS;
+    for (int e = threadIdx.x; e < E; e += ST_T) {
+        const int64_t r = b - H + e;
+        const bool in = r >= 0 && r < n;
+        xs[spad(e)] = in ? nan_if_inf(x[r]) : (double)NAN;
+        is[spad(e)] = in ? ids[r] : 0;
+    }
+    __syncthreads();
+    const int e0 = H + threadIdx.x * ST_R;   // halo index of this thread's first row
+    const int64_t i0 = b + threadIdx.x * ST_R;
+    if (i0 >= n) return;
+    const int64_t id0 = is[spad(e0)];
+    // first window: rows max(i0 - H, firm start)..i0, direct two-pass
+    const int lo = (int)(i0 - H >= 0 ? e0 - H : e0 - i0);
+    int cnt = 0, run = 0;
+    double sum = 0.0, last = NAN;
+    for (int e = lo; e <= e0; ++e) {
+        const double v = xs[spad(e)];
+        if (is[spad(e)] != id0 || isnan(v)) continue;
+        ++cnt;
+        sum += v;
+        run = v == last ? run + 1 : 1;
+        last = v;
+    }
+    double mean = cnt > 0 ? sum / (double)cnt : 0.0, m2 = 0.0;
+    for (int e = lo; e <= e0; ++e) {
+        const double v = xs[spad(e)];
+        if (is[spad(e)] != id0 || isnan(v)) continue;
+        const double d = v - mean;
+        m2 += d * d;
+    }
+    const int need = minp > 2 ? minp : 2;
+    for (int r = 0; r < ST_R; ++r) {
+        const int64_t i = i0 + r;
+        if (i >= n) break;
+        const int e = e0 + r;
+        if (r > 0) {
+            const int64_t id = is[spad(e)];
+            if (id != is[spad(e - 1)]) {   // a new firm starts here
+                cnt = 0;
+                run = 0;
+                mean = 0.0;
+                m2 = 0.0;
+                last = NAN;
+            } else if (i - W >= 0 && is[spad(e - W)] == id) {   // row i - W leaves the window
+                const double v = xs[spad(e - W)];
+                if (!isnan(v)) {
+                    --cnt;
+                    if (cnt == 0) {
+                        mean = 0.0;
+                        m2 = 0.0;
+                    } else {
+                        const double d = v - mean;
+                        mean -= d / (double)cnt;
+                        m2 -= d * (v - mean);
+                    }
+                }
+            }
+            const double v = xs[spad(e)];
+            if (!isnan(v)) {
+                ++cnt;
+                const double d = v - mean;
+                mean += d / (double)cnt;
+                m2 += d * (v - mean);
+                run = v == last ? run + 1 : 1;
+                last = v;
+            }
+        }
+        double res = NAN;
+        if (cnt >= need) {
+            if (run >= cnt) {
+                res = 0.0;   // pandas: every observation in the window is the same value
+            } else {
+                const double var = m2 / (double)(cnt - 1);
+                res = sqrt(var > 0.0 ? var : 0.0) * scale;
+            }
+        }
+        out[i] = res;
+    }
+}
+
+}  // namespace
+}  // namespace fm
+
+extern "C" int fm_firm_chars(const fm_chars_args* args, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(args != nullptr, "fm_firm_chars: null args");
+    const fm_chars_args& a = *args;
+    FM_REQUIRE(a.n >= 0, "fm_firm_chars: negative n");
+    if (a.n == 0) return FM_OK;
+    FM_REQUIRE(a.ids != nullptr, "fm_firm_chars: null ids");
+    // fields each characteristic reads (FM_CHAR_* order)
+    static const uint32_t need[FM_NCHARS] = {
+        1u << FM_FIELD_ME,
+        (1u << FM_FIELD_ME) | (1u << FM_FIELD_BE),
+        1u << FM_FIELD_RETX,
+        (1u << FM_FIELD_ACCRUALS) | (1u << FM_FIELD_DEPRECIATION),
+        (1u << FM_FIELD_EARNINGS) | (1u << FM_FIELD_ASSETS),
+        1u << FM_FIELD_ASSETS,
+        (1u << FM_FIELD_DVC) | (1u << FM_FIELD_PRC),
+        1u << FM_FIELD_RETX,
+        1u << FM_FIELD_SHROUT,
+        1u << FM_FIELD_SHROUT,
+        (1u << FM_FIELD_ME) | (1u << FM_FIELD_TOTAL_DEBT),
+        (1u << FM_FIELD_ME) | (1u << FM_FIELD_SALES),
+    };
+    uint32_t req = 0;
+    for (int c = 0; c < FM_NCHARS; ++c)
+        if (a.out[c]) req |= need[c];
+    if (req == 0) return FM_OK;
+    for (int f = 0; f < FM_NFIELDS; ++f)
+        FM_REQUIRE(!((req >> f) & 1u) || a.field[f] != nullptr, "fm_firm_chars: field %d required but NULL", f);
+    const int need_ret = (a.out[FM_CHAR_RETURN_12_2] || a.out[FM_CHAR_LOG_RETURN_13_36]) ? 1 : 0;
+    const int need_dvc = a.out[FM_CHAR_DY] ? 1 : 0;
+    const int64_t blocks = (a.n + CT - 1) / CT;
+    FM_REQUIRE(blocks < (1ll << 31), "fm_firm_chars: too many rows");
+    hipLaunchKernelGGL(firm_chars_kernel, dim3((unsigned)blocks), dim3(CT), 0, (hipStream_t)stream, a,
+                       need_ret, need_dvc);
+    FM_CHECK_LAUNCH("fm_firm_chars");
+    return FM_OK;
+}
+
+extern "C" int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, int32_t window,
+                              int32_t min_periods, double scale, double* out, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(n >= 0, "fm_rolling_std: negative n");
+    if (n == 0) return FM_OK;
+    FM_REQUIRE(ids && x && out, "fm_rolling_std: null pointer");
+    FM_REQUIRE(window >= 1 && window <= 4096, "fm_rolling_std: window must be 1..4096");
+    FM_REQUIRE(min_periods >= 1 && min_periods <= window, "fm_rolling_std: min_periods must be 1..window");
+    const int E = ST_ROWS + window - 1;
+    const size_t lds = (size_t)(spad(E) + 1) * 8 * 2;
+    FM_REQUIRE(lds <= 160 * 1024, "fm_rolling_std: window too large for LDS");
+    const int64_t blocks = (n + ST_ROWS - 1) / ST_ROWS;
+    FM_REQUIRE(blocks < (1ll << 31), "fm_rolling_std: too many rows");
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)rolling_std_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess) {
+        set_error("fm_rolling_std: cannot raise the dynamic LDS limit to %zu bytes", lds);
+        return FM_EHIP;
+    }
+    hipLaunchKernelGGL(rolling_std_kernel, dim3((unsigned)blocks), dim3(ST_T), lds, (hipStream_t)stream, ids,
+                       x, n, (int)window, (int)min_periods, scale, out);
+    FM_CHECK_LAUNCH("fm_rolling_std");
+    return FM_OK;
+}

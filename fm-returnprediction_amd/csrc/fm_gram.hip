@@ -93,7 +93,9 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);   // wave-uniform (SGPR loops)
-    const int chunk = blockIdx.x;
+    // chunks run last-month-first: fm_select streams the panel month by month, so the
+    // months it read last are still in the memory-side cache when they are read here
+    const int chunk = (int)gridDim.x - 1 - (int)blockIdx.x;
     const int seg = a.chunk_seg[chunk];
     const int64_t r0 = a.chunk_row[2 * chunk], r1 = a.chunk_row[2 * chunk + 1];
     const int ncols = a.ncols, nseg = a.nseg, nmodels = a.nmodels, nlevels = a.nlevels;

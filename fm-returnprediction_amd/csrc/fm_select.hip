@@ -602,6 +602,11 @@ __device__ __forceinline__ void pick_tail(const double* L, int c, int ra, int rb
     vb = rb < c ? at(rb) : tau;
 }
 
+__device__ __forceinline__ int64_t unit_of(const SelArgs& a, int64_t k) {
+    const int64_t s = k / a.ncols, c = k - s * a.ncols;
+    return c * a.nseg + s;
+}
+
 // Issue the loads of unit u into xv (no value is used here: clamped 32-bit byte offsets,
 // masking happens at use, so the loads stay in flight while the caller keeps working).
 template <int VPL>
@@ -636,8 +641,13 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
     const int64_t nunits = (int64_t)a.nseg * a.ncols;
     const int64_t nwt = (int64_t)gridDim.x * SNW;
-    int64_t u = (int64_t)blockIdx.x * SNW + w;
-    if (u >= nunits) return;   // wave-uniform; no block barriers below
+    // Work order is month-major (k -> month k / ncols, column k % ncols) so the panel is
+    // streamed month by month, the order fm_gram then reads back in reverse (its first
+    // months are this kernel's last, still in the memory-side cache); outputs stay indexed
+    // by u = column * nseg + month.
+    int64_t k = (int64_t)blockIdx.x * SNW + w;
+    if (k >= nunits) return;   // wave-uniform; no block barriers below
+    int64_t u = unit_of(a, k);
     const bool early = a.mean == nullptr;   // prefetch right after compaction
     double xv[VPL];
     int L = load_unit<VPL>(a, u, xv);
@@ -645,8 +655,9 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
     double* Ll = cbuf[w][0];
     double* Lh = cbuf[w][1];
     while (true) {
-        const int64_t un = u + nwt;
-        const bool more = un < nunits;
+        const int64_t kn = k + nwt;
+        const bool more = kn < nunits;
+        const int64_t un = more ? unit_of(a, kn) : 0;
         int Ln = 0;
         // min / max with 4 independent accumulators each (the chains would otherwise serialize
         // on the f64 latency)
@@ -810,6 +821,7 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
         }
         if (!more) break;
         if (!early) Ln = load_unit<VPL>(a, un, xv);
+        k = kn;
         u = un;
         L = Ln;
     }

@@ -75,6 +75,14 @@ class SolveArgs(C.Structure):
     ]
 
 
+FM_NFIELDS = 12
+FM_NCHARS = 12
+
+
+class CharsArgs(C.Structure):
+    _fields_ = [("ids", _p), ("n", _i64), ("field", _p * FM_NFIELDS), ("out", _p * FM_NCHARS)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "fm_version": (C.c_char_p, []),
@@ -105,6 +113,8 @@ _SIGS = {
     "fm_forecast": (_i32, [_p, _i64, _i32, _p, _i32, _i64, _p, _i32, _p, _p]),
     "fm_segment_moments": (_i32, [_p, _i64, _i32, _p, _i32, _p, _i32, _i32, _p, _p, _p, _p]),
     "fm_distinct_count": (_i32, [_p, _i64, _p, _i64, _i32, _p, _i32, _i32, _i64, _i64, _p, _p, _p]),
+    "fm_firm_chars": (_i32, [C.POINTER(CharsArgs), _p]),
+    "fm_rolling_std": (_i32, [_p, _p, _i64, _i32, _i32, _f64, _p, _p]),
     "fm_gen_panel": (_i32, [C.c_uint64, _i64, _i32, _i32, _f64, _f64, _p, _i64, _p, _p, _p]),
     "fm_stream_probe": (_i32, [_p, _i64, _p, _p]),
 }

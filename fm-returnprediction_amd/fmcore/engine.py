@@ -739,6 +739,51 @@ def distinct_count(ids, cols, level=None, min_level=0, finite_only=True):
     return out
 
 
+# ------------------------------------------------------------------------------------------
+# Firm-axis characteristics (src/calc_Lewellen_2014.py:137-466)
+# ------------------------------------------------------------------------------------------
+CHAR_FIELDS = ("me", "be", "retx", "accruals", "depreciation", "earnings", "assets", "dvc", "prc",
+               "shrout", "total_debt", "sales")
+CHAR_NAMES = ("log_size", "log_bm", "return_12_2", "accruals_final", "roa", "log_assets_growth",
+              "dy", "log_return_13_36", "log_issues_12", "log_issues_36", "debt_price", "sales_price")
+
+
+def firm_chars(ids, fields, names=CHAR_NAMES, out=None):
+    """Monthly characteristics for FIRM-major rows (each firm's rows contiguous, in frame
+    order).  ``ids`` int64 [n]; ``fields`` maps CHAR_FIELDS names -> float64 [n] device
+    tensors (only those the requested characteristics read); returns {name: float64 [n]}.
+    ``out`` (optional) is a [len(names), n] float64 tensor to write into."""
+    n = int(ids.shape[0])
+    dev = ids.device
+    if out is None:
+        out = torch.empty((len(names), n), dtype=torch.float64, device=dev)
+    a = L.CharsArgs()
+    a.ids = ids.data_ptr()
+    a.n = n
+    keep = [ids, out]
+    for f, nm in enumerate(CHAR_FIELDS):
+        t = fields.get(nm)
+        if t is not None:
+            t = t.contiguous()
+            keep.append(t)
+            a.field[f] = t.data_ptr()
+    for j, nm in enumerate(names):
+        a.out[CHAR_NAMES.index(nm)] = out[j].data_ptr()
+    _remember("fm_firm_chars", "fm_firm_chars", a, *keep)
+    _kcall("fm_firm_chars", "fm_firm_chars", L.C.byref(a), _stream())
+    return {nm: out[j] for j, nm in enumerate(names)}
+
+
+def rolling_std(ids, x, window=252, min_periods=100, scale=252 ** 0.5, out=None):
+    """Per-row rolling std (ddof=1) over the last ``window`` rows of each firm group."""
+    n = int(x.shape[0])
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=x.device)
+    _kcall("fm_rolling_std", "fm_rolling_std", ids.data_ptr(), x.data_ptr(), n, int(window),
+           int(min_periods), float(scale), out.data_ptr(), _stream())
+    return out
+
+
 def stream_probe(t):
     out = torch.zeros(1, dtype=torch.float64, device=t.device)
     _kcall("fm_stream_probe", "fm_stream_probe", t.data_ptr(), t.numel(), out.data_ptr(), _stream())

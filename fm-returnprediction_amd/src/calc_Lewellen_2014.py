@@ -10,8 +10,14 @@ Mirrored (same names, signatures, return types and row/column/index order):
 Extensions the north star names (not in the reference; parity unpinned):
   standardize, monthly_coefficients, rolling_coefficients, expected_return_forecasts,
   predictive_slope_regressions, lewellen_pipeline.
-The firm-characteristic builders (calc_*), data pulls and LaTeX output of the reference are
-outside this drop-in (scope).
+Firm-axis characteristic builders (§8(f) row 2; one fused device pass, fm_firm_chars):
+  calc_log_size, calc_log_bm, calc_return_12_2, calc_accruals, calc_roa,
+  calc_log_assets_growth, calc_dy, calc_log_return_13_36, calc_log_issues_12,
+  calc_log_issues_36, calc_debt_price, calc_sales_price   reference :137-341
+  calc_std_12      reference :438-466   252-day rolling std on device (fm_rolling_std)
+  calc_characteristics (extension): all twelve monthly characteristics in one launch.
+Data pulls, the polars weekly beta (calculate_rolling_beta, :344-435) and LaTeX output of
+the reference are outside this drop-in (scope).
 """
 import os
 import sys
@@ -128,6 +134,153 @@ def standardize(crsp_comp: pd.DataFrame, varlist: list, date_col: str = "mthcald
         col[panel.order] = z[i]
         df[v] = col
     return df
+
+
+# ------------------------------------------------------------------------------------------
+# Firm-axis characteristics (reference :137-466)
+# ------------------------------------------------------------------------------------------
+def _firm_grouping(permno):
+    """groupby("permno") row order: each firm's rows contiguous, frame order inside a firm
+    (a stable sort by permno; None when the frame is already grouped that way)."""
+    ids = np.asarray(permno, dtype=np.int64)
+    if len(ids) < 2 or bool(np.all(ids[1:] >= ids[:-1])):
+        return ids, None
+    order = np.argsort(ids, kind="stable")
+    return ids[order], order
+
+
+def _device_chars(df, names):
+    """{name: float64 ndarray in df's row order} for the requested characteristics."""
+    import torch
+    dev = _E.require_device()
+    ids, order = _firm_grouping(df["permno"].to_numpy())
+    reads = set()
+    for nm in names:
+        reads |= _CHAR_READS[nm]
+    fields = {}
+    for f in reads:
+        v = _api.as_f64(df[f])
+        fields[f] = torch.from_numpy(np.ascontiguousarray(v if order is None else v[order])).to(dev)
+    out = _E.firm_chars(torch.from_numpy(ids).to(dev), fields, names)
+    res = {}
+    for nm in names:
+        v = out[nm].cpu().numpy()
+        if order is not None:
+            u = np.empty_like(v)
+            u[order] = v
+            v = u
+        res[nm] = v
+    return res
+
+
+_CHAR_READS = {
+    "log_size": {"me"}, "log_bm": {"me", "be"}, "return_12_2": {"retx"},
+    "accruals_final": {"accruals", "depreciation"}, "roa": {"earnings", "assets"},
+    "log_assets_growth": {"assets"}, "dy": {"dvc", "prc"}, "log_return_13_36": {"retx"},
+    "log_issues_12": {"shrout"}, "log_issues_36": {"shrout"}, "debt_price": {"me", "total_debt"},
+    "sales_price": {"me", "sales"},
+}
+
+
+def _add_char(crsp_comp, name):
+    crsp_comp[name] = _device_chars(crsp_comp, [name])[name]
+    return crsp_comp
+
+
+def calc_log_size(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """log(me) of the firm's previous row (reference :137-147)."""
+    return _add_char(crsp_comp, "log_size")
+
+
+def calc_log_bm(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """log(be[t-1]) - log(me[t-1]) (reference :150-163)."""
+    return _add_char(crsp_comp, "log_bm")
+
+
+def calc_return_12_2(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """prod(1 + retx) over the firm's rows t-12..t-2, all 11 present, minus 1 (:166-192)."""
+    return _add_char(crsp_comp, "return_12_2")
+
+
+def calc_accruals(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """accruals - depreciation (reference :195-204)."""
+    return _add_char(crsp_comp, "accruals_final")
+
+
+def calc_roa(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """earnings / assets (reference :241-249)."""
+    return _add_char(crsp_comp, "roa")
+
+
+def calc_log_assets_growth(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """log(assets / assets twelve firm rows back) (reference :252-262)."""
+    return _add_char(crsp_comp, "log_assets_growth")
+
+
+def calc_dy(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """Sum of dvc over the firm's last 12 rows (min_periods=1) / prc[t-1], on a copy sorted by
+    [permno, mthcaldt], which is returned (reference :265-287)."""
+    df = crsp_comp.sort_values(["permno", "mthcaldt"]).copy()
+    return _add_char(df, "dy")
+
+
+def calc_log_return_13_36(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """Sum of log(1 + retx) over the firm's rows t-36..t-13, all 24 present (:290-313)."""
+    return _add_char(crsp_comp, "log_return_13_36")
+
+
+def calc_log_issues_12(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """log(shrout[t-1]) - log(shrout[t-12]) (reference :224-238)."""
+    return _add_char(crsp_comp, "log_issues_12")
+
+
+def calc_log_issues_36(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """log(shrout[t-1]) - log(shrout[t-36]) (reference :207-221)."""
+    return _add_char(crsp_comp, "log_issues_36")
+
+
+def calc_debt_price(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """total_debt / me[t-1] (reference :316-327)."""
+    return _add_char(crsp_comp, "debt_price")
+
+
+def calc_sales_price(crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """sales / me[t-1] (reference :330-341)."""
+    return _add_char(crsp_comp, "sales_price")
+
+
+def calc_characteristics(crsp_comp: pd.DataFrame, names=None) -> pd.DataFrame:
+    """Extension: the twelve monthly characteristics in get_factors order (reference
+    :537-547) from ONE device pass; same values as calling the calc_* one by one on a frame
+    sorted by [permno, mthcaldt] (calc_dy's re-sort is then a no-op)."""
+    names = list(_E.CHAR_NAMES if names is None else names)
+    out = _device_chars(crsp_comp, names)
+    for nm in names:
+        crsp_comp[nm] = out[nm]
+    return crsp_comp
+
+
+def calc_std_12(crsp_d: pd.DataFrame, crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """Annualized 252-day rolling std of daily retx per permno (min_periods=100), the last
+    day of each (permno, month), left-merged onto crsp_comp on [permno, jdate]
+    (reference :438-466).  The rolling std runs on device; the month-end pick and the merge
+    are the reference's pandas steps."""
+    import torch
+    dev = _E.require_device()
+    df_std_12 = crsp_d.copy()
+    ids, order = _firm_grouping(df_std_12["permno"].to_numpy())
+    x = _api.as_f64(df_std_12["retx"])
+    xs = torch.from_numpy(np.ascontiguousarray(x if order is None else x[order])).to(dev)
+    sd = _E.rolling_std(torch.from_numpy(ids).to(dev), xs, 252, 100, float(np.sqrt(252))).cpu().numpy()
+    if order is not None:
+        u = np.empty_like(sd)
+        u[order] = sd
+        sd = u
+    df_std_12["rolling_std_252"] = sd
+    df_std_12["jdate"] = df_std_12["dlycaldt"].dt.to_period("M").dt.to_timestamp("M")
+    df_std_12.drop_duplicates(subset=["permno", "jdate"], keep="last", inplace=True)
+    return pd.merge(left=crsp_comp, right=df_std_12[["permno", "jdate", "rolling_std_252"]],
+                    on=["permno", "jdate"], how="left")
 
 
 # ------------------------------------------------------------------------------------------

@@ -37,6 +37,12 @@
  *   fm_forecast     <- build-defined extension A7: per-row F = a_{t-1} + b_{t-1}'x_t
  *   fm_segment_moments, fm_distinct_count <- build_table_1's monthly mean / std(ddof=1)
  *                      and permno nunique (src/calc_Lewellen_2014.py:623-646)
+ *   fm_firm_chars   <- get_factors' twelve monthly characteristics: groupby("permno")
+ *                      .shift(k) lags, rolling(11).apply(np.prod), rolling(12).sum(),
+ *                      rolling(24).sum() and the log / ratio arithmetic of calc_log_size ..
+ *                      calc_sales_price (src/calc_Lewellen_2014.py:137-341, called at :537-548)
+ *   fm_rolling_std  <- calc_std_12's groupby("permno")["retx"].rolling(252,
+ *                      min_periods=100).std() * sqrt(252) (src/calc_Lewellen_2014.py:448-456)
  *   fm_gen_panel    <- (bench/test data) counter-based synthetic panel, bit-identical to
  *                      fmcore/synth.py
  *
@@ -264,6 +270,56 @@ int fm_distinct_count(const int64_t* ids, int64_t nrows, const double* cols, int
                       int32_t ncols, const uint8_t* level, int32_t min_level, int32_t finite_only,
                       int64_t id_lo, int64_t id_range, uint32_t* bitmap, int32_t* out,
                       void* stream);
+
+/* Firm-axis characteristic construction.  Rows are FIRM-major:
+ * grouped by firm id (each firm's rows contiguous, in the reference frame's order inside the
+ * group — get_factors sorts by (permno, mthcaldt), src/calc_Lewellen_2014.py:533).  Row i's
+ * lag-k value exists iff ids[i-k] == ids[i].  field[f] / out[c] are device columns of n
+ * doubles indexed by FM_FIELD_* / FM_CHAR_*; out[c] == NULL skips characteristic c, and a
+ * requested characteristic needs its fields non-NULL (else FM_EINVAL).  Rolling windows turn
+ * +-inf into NaN first (pandas _prep_values). */
+#define FM_NFIELDS 12
+#define FM_FIELD_ME 0
+#define FM_FIELD_BE 1
+#define FM_FIELD_RETX 2
+#define FM_FIELD_ACCRUALS 3
+#define FM_FIELD_DEPRECIATION 4
+#define FM_FIELD_EARNINGS 5
+#define FM_FIELD_ASSETS 6
+#define FM_FIELD_DVC 7
+#define FM_FIELD_PRC 8
+#define FM_FIELD_SHROUT 9
+#define FM_FIELD_TOTAL_DEBT 10
+#define FM_FIELD_SALES 11
+
+#define FM_NCHARS 12
+#define FM_CHAR_LOG_SIZE 0          /* log(me[t-1])                       :137-147 */
+#define FM_CHAR_LOG_BM 1            /* log(be[t-1]) - log(me[t-1])        :150-163 */
+#define FM_CHAR_RETURN_12_2 2       /* prod(1 + retx[t-12..t-2]) - 1      :166-192 */
+#define FM_CHAR_ACCRUALS_FINAL 3    /* accruals - depreciation            :195-204 */
+#define FM_CHAR_ROA 4               /* earnings / assets                  :241-249 */
+#define FM_CHAR_LOG_ASSETS_GROWTH 5 /* log(assets / assets[t-12])         :252-262 */
+#define FM_CHAR_DY 6                /* sum(dvc[t-11..t], minp 1) / prc[t-1] :265-287 */
+#define FM_CHAR_LOG_RETURN_13_36 7  /* sum(log(1 + retx[t-36..t-13]))     :290-313 */
+#define FM_CHAR_LOG_ISSUES_12 8     /* log(shrout[t-1]) - log(shrout[t-12]) :224-238 */
+#define FM_CHAR_LOG_ISSUES_36 9     /* log(shrout[t-1]) - log(shrout[t-36]) :207-221 */
+#define FM_CHAR_DEBT_PRICE 10       /* total_debt / me[t-1]               :316-327 */
+#define FM_CHAR_SALES_PRICE 11      /* sales / me[t-1]                    :330-341 */
+
+typedef struct fm_chars_args {
+    const int64_t* ids;                 /* [n] firm id per row (grouped)                 */
+    int64_t n;
+    const double* field[FM_NFIELDS];    /* FM_FIELD_* columns, NULL if absent           */
+    double* out[FM_NCHARS];             /* FM_CHAR_* outputs, NULL = not computed       */
+} fm_chars_args;
+
+int fm_firm_chars(const fm_chars_args* args, void* stream);
+
+/* Per-row rolling std (ddof=1) over the last `window` rows of each firm group (rows grouped
+ * as for fm_firm_chars), NaN below `min_periods` observations, exactly 0 when all
+ * observations are equal, times `scale`.  1 <= window <= 4096, 2 <= min_periods <= window. */
+int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, int32_t window,
+                   int32_t min_periods, double scale, double* out, void* stream);
 
 int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
                  double nan_rate, double nyse_rate, double* cols, int64_t col_stride,

@@ -80,3 +80,17 @@ def frame_from(npz, prefix):
             v = v.astype(bool)
         data[c] = v
     return pd.DataFrame(data, index=pd.Index(npz[prefix + "index"]))
+
+
+def chars_inputs(g):
+    """The raw monthly / daily golden input frames of chars.npz (tests/golden/cases.py)."""
+    import pandas as pd
+    m = pd.DataFrame({"permno": g["in_permno"], "mthcaldt": g["in_mthcaldt"].astype("datetime64[ns]")},
+                     index=pd.Index(g["in_index"]))
+    for k in ("me", "be", "retx", "accruals", "depreciation", "earnings", "assets", "dvc", "prc",
+              "shrout", "total_debt", "sales"):
+        m[k] = g["in_" + k]
+    m["jdate"] = m["mthcaldt"]
+    d = pd.DataFrame({"permno": g["din_permno"], "dlycaldt": g["din_dlycaldt"].astype("datetime64[ns]"),
+                      "retx": g["din_retx"]}, index=pd.Index(g["din_index"]))
+    return m, d

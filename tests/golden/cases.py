@@ -195,3 +195,93 @@ def percentile_arrays():
             v[rng.random(n) < 0.03] = -np.inf
         arrs.append(v)
     return arrs
+
+
+# ------------------------------------------------------------------------------------------
+# Firm-axis characteristic construction: raw monthly CRSP/Compustat
+# fields and daily returns, before get_factors (src/calc_Lewellen_2014.py:531-575).
+# ------------------------------------------------------------------------------------------
+RAW_FIELDS = ["me", "be", "retx", "accruals", "depreciation", "earnings", "assets", "dvc", "prc",
+              "shrout", "total_debt", "sales"]
+CHAR_NAMES = ["log_size", "log_bm", "return_12_2", "accruals_final", "roa", "log_assets_growth",
+              "dy", "log_return_13_36", "log_issues_12", "log_issues_36", "debt_price", "sales_price"]
+
+
+def raw_monthly_panel(nfirms=70, nmonths=60, seed=21, shuffle=True):
+    """Ragged firm histories (1..60 rows, random starts, 5% dropped months), NaNs, zeros,
+    negatives and infinities in the fields the characteristics take logs / ratios of."""
+    rng = np.random.default_rng(seed)
+    months = pd.date_range("2001-01-31", periods=nmonths, freq=pd.offsets.MonthEnd())
+    parts = []
+    for f in range(nfirms):
+        start = int(rng.integers(0, nmonths))
+        length = int(rng.integers(1, nmonths - start + 1))
+        if f % 7 == 0:
+            start, length = 0, nmonths                      # long histories (all windows fill)
+        idx = np.arange(start, start + length)
+        idx = idx[rng.random(len(idx)) > 0.05] if len(idx) > 3 else idx
+        n = len(idx)
+        if n == 0:
+            continue
+        d = {"permno": np.full(n, 10000 + 7 * f, dtype=np.int64), "mthcaldt": months[idx]}
+        d["me"] = np.exp(rng.normal(5, 2, n))
+        d["be"] = d["me"] * np.exp(rng.normal(-0.5, 0.8, n))
+        d["retx"] = rng.standard_t(4, n) * 0.08
+        d["accruals"] = rng.normal(0.0, 0.05, n)
+        d["depreciation"] = np.abs(rng.normal(0.03, 0.01, n))
+        d["earnings"] = rng.normal(0.02, 0.1, n) * 100
+        d["assets"] = np.exp(rng.normal(6, 1.5, n))
+        d["dvc"] = np.where(rng.random(n) < 0.7, 0.0, np.abs(rng.normal(0.5, 0.3, n)))
+        d["prc"] = np.exp(rng.normal(3, 1, n)) * np.where(rng.random(n) < 0.05, -1.0, 1.0)
+        d["shrout"] = np.exp(rng.normal(9, 1, n)) * np.exp(np.cumsum(rng.normal(0, 0.01, n)))
+        d["total_debt"] = np.abs(rng.normal(100, 60, n))
+        d["sales"] = np.abs(rng.normal(300, 200, n))
+        for k in RAW_FIELDS:
+            d[k][rng.random(n) < 0.03] = np.nan
+        parts.append(pd.DataFrame(d))
+    df = pd.concat(parts, ignore_index=True)
+    # edge values: log(0) = -inf, log(<0) = NaN, 1 + retx = 0, +-inf returns and fields
+    df.loc[df.index[5], "me"] = 0.0
+    df.loc[df.index[40], "be"] = -3.0
+    long_rows = df.index[df["permno"] == 10000]
+    df.loc[long_rows[20], "retx"] = -1.0
+    df.loc[long_rows[45], "retx"] = np.inf
+    long2 = df.index[df["permno"] == 10000 + 7 * 7]
+    df.loc[long2[30], "dvc"] = np.inf
+    df.loc[long2[10:14], "dvc"] = np.nan                   # dy over an all-NaN stretch
+    df.loc[long2[33], "shrout"] = -np.inf
+    df.loc[long2[50], "assets"] = 0.0
+    df["jdate"] = df["mthcaldt"]
+    if shuffle:
+        df = df.iloc[rng.permutation(len(df))]
+        df.index = pd.Index(rng.permutation(len(df)) * 2 + 500)
+    return df
+
+
+def raw_daily_panel(nfirms=14, ndays=700, seed=22, shuffle=True):
+    """Daily returns for calc_std_12 (src/calc_Lewellen_2014.py:438-466): ragged histories
+    (some shorter than the 100-day minimum), NaN stretches, infinities and a long run of one
+    repeated value (pandas reports an exact 0 std there)."""
+    rng = np.random.default_rng(seed)
+    days = pd.bdate_range("2001-01-02", periods=ndays)
+    parts = []
+    for f in range(nfirms):
+        start = 0 if f % 3 == 0 else int(rng.integers(0, ndays - 50))
+        length = ndays - start if f % 3 == 0 else int(rng.integers(50, ndays - start + 1))
+        idx = np.arange(start, start + length)
+        n = len(idx)
+        r = rng.normal(0.0005, 0.02, n)
+        r[rng.random(n) < 0.02] = np.nan
+        if f == 0:
+            r[300:420] = 0.0                               # 120 equal values
+            r[100:130] = np.nan
+        if f == 3:
+            r[200] = np.inf
+            r[450] = -np.inf
+        parts.append(pd.DataFrame({"permno": np.full(n, 10000 + 7 * f, dtype=np.int64),
+                                   "dlycaldt": days[idx], "retx": r}))
+    df = pd.concat(parts, ignore_index=True)
+    if shuffle:
+        df = df.iloc[rng.permutation(len(df))]
+        df.index = pd.Index(rng.permutation(len(df)) + 10)
+    return df

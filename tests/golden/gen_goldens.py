@@ -302,6 +302,68 @@ def gen_pct():
                         qs=np.array(qs, dtype=float), np_percentile=res, pd_quantile=pdq)
 
 
+CHAR_FUNCS = ["calc_log_size", "calc_log_bm", "calc_return_12_2", "calc_accruals", "calc_roa",
+              "calc_log_assets_growth", "calc_dy", "calc_log_return_13_36", "calc_log_issues_12",
+              "calc_log_issues_36", "calc_debt_price", "calc_sales_price"]
+
+
+def load_chars():
+    """The firm-axis characteristic functions of get_factors (src/calc_Lewellen_2014.py:137-466),
+    AST-extracted like load_calc (the module's polars/wrds imports are absent here)."""
+    src = open(os.path.join(REF, "calc_Lewellen_2014.py")).read()
+    keep = set(CHAR_FUNCS) | {"calc_std_12"}
+    fns = [n for n in ast.parse(src).body if isinstance(n, ast.FunctionDef) and n.name in keep]
+    ns = dict(np=np, pd=pd)
+    exec(compile(ast.Module(fns, []), "calc_Lewellen_2014.py", "exec"), ns)
+    return ns
+
+
+def gen_chars():
+    """Each calc_* on a scrambled raw panel (groupby order = frame order), the get_factors
+    chain (sorted by permno, date; :531-548 without the polars beta), and calc_std_12."""
+    ns = load_chars()
+    d = {}
+    base = cases.raw_monthly_panel()
+    daily = cases.raw_daily_panel()
+    d["in_index"] = base.index.values.astype(np.int64)
+    d["in_permno"] = base["permno"].values.astype(np.int64)
+    d["in_mthcaldt"] = base["mthcaldt"].values.astype("datetime64[ns]").astype(np.int64)
+    for k in cases.RAW_FIELDS:
+        d["in_" + k] = base[k].values.astype(np.float64)
+    d["din_index"] = daily.index.values.astype(np.int64)
+    d["din_permno"] = daily["permno"].values.astype(np.int64)
+    d["din_dlycaldt"] = daily["dlycaldt"].values.astype("datetime64[ns]").astype(np.int64)
+    d["din_retx"] = daily["retx"].values.astype(np.float64)
+    for fn, col in zip(CHAR_FUNCS, cases.CHAR_NAMES):
+        out = ns[fn](base.copy())
+        d[f"single_{col}_index"] = out.index.values.astype(np.int64)
+        d[f"single_{col}"] = out[col].values.astype(np.float64)
+        d[f"single_{col}_columns"] = np.array(list(out.columns))
+    # get_factors order (:533-548)
+    cc = base.sort_values(["permno", "mthcaldt"])
+    dd = daily.sort_values(["permno", "dlycaldt"])
+    for fn in CHAR_FUNCS:
+        cc = ns[fn](cc)
+    cc = ns["calc_std_12"](dd, cc)
+    d["chain_index"] = cc.index.values.astype(np.int64)
+    d["chain_columns"] = np.array(list(cc.columns))
+    d["chain_permno"] = cc["permno"].values.astype(np.int64)
+    d["chain_mthcaldt"] = cc["mthcaldt"].values.astype("datetime64[ns]").astype(np.int64)
+    for col in cases.CHAR_NAMES + ["rolling_std_252"]:
+        d["chain_" + col] = cc[col].values.astype(np.float64)
+    # calc_std_12 on scrambled inputs (rolling in frame order within permno; left merge)
+    s12 = ns["calc_std_12"](daily.copy(), base.copy())
+    d["std_index"] = s12.index.values.astype(np.int64)
+    d["std_permno"] = s12["permno"].values.astype(np.int64)
+    d["std_mthcaldt"] = s12["mthcaldt"].values.astype("datetime64[ns]").astype(np.int64)
+    d["std_rolling_std_252"] = s12["rolling_std_252"].values.astype(np.float64)
+    # the per-day rolling std itself (before the month-end pick and the merge)
+    dsort = daily.sort_values(["permno", "dlycaldt"])
+    r = dsort.groupby("permno")["retx"].rolling(window=252, min_periods=100).std()
+    d["daily_std_sorted"] = r.reset_index(level=0, drop=True).reindex(dsort.index).values * np.sqrt(252)
+    np.savez_compressed(os.path.join(HERE, "chars.npz"), **d)
+
+
 if __name__ == "__main__":
     print("numpy", np.__version__, "pandas", pd.__version__, "statsmodels", sm.__version__ if hasattr(sm, "__version__") else "?")
     gen_pct()
@@ -312,4 +374,5 @@ if __name__ == "__main__":
     gen_fig1()
     gen_mid()
     gen_table1()
+    gen_chars()
     print("ok")

@@ -360,3 +360,124 @@ def test_table1_golden(CL):
     for r, row in enumerate(g["values"]):
         for c, v in enumerate(row):
             assert scalar_close(t1.values[r, c], v, 1e-12), (g["index"][r], g["columns"][c])
+
+
+# ---------------------------------------------------------------- firm-axis characteristics
+from oracle import chars_oracle as CO  # noqa: E402
+from fmtol import chars_inputs  # noqa: E402
+
+_CHAR_FUNCS = ["calc_log_size", "calc_log_bm", "calc_return_12_2", "calc_accruals", "calc_roa",
+               "calc_log_assets_growth", "calc_dy", "calc_log_return_13_36", "calc_log_issues_12",
+               "calc_log_issues_36", "calc_debt_price", "calc_sales_price"]
+
+
+def test_chars_single_golden(CL):
+    """Each calc_* on a scrambled frame (groupby order = frame order) vs the reference."""
+    g = load_npz("chars.npz")
+    m, _ = chars_inputs(g)
+    for fn, col in zip(_CHAR_FUNCS, CO.CHARS):
+        out = getattr(CL, fn)(m.copy())
+        assert np.array_equal(out.index.values, g[f"single_{col}_index"]), fn
+        assert list(out.columns) == list(g[f"single_{col}_columns"]), fn
+        assert_series_close(out[col].values, g[f"single_{col}"], fn)
+
+
+def test_chars_chain_golden(CL):
+    """get_factors' order (sorted, twelve characteristics, calc_std_12) vs the reference;
+    calc_characteristics (one launch) must equal the per-function chain."""
+    g = load_npz("chars.npz")
+    m, d = chars_inputs(g)
+    ms = m.sort_values(["permno", "mthcaldt"])
+    ds = d.sort_values(["permno", "dlycaldt"])
+    one = CL.calc_characteristics(ms.copy())
+    cc = ms.copy()
+    for fn in _CHAR_FUNCS:
+        cc = getattr(CL, fn)(cc)
+    for col in CO.CHARS:
+        assert _same(one[col].values, cc[col].values), col
+    cc = CL.calc_std_12(ds, cc)
+    assert list(cc.columns) == list(g["chain_columns"])
+    assert np.array_equal(cc.index.values, g["chain_index"])
+    for col in CO.CHARS + ["rolling_std_252"]:
+        assert_series_close(cc[col].values, g["chain_" + col], col)
+
+
+def test_std_12_scrambled_golden(CL):
+    g = load_npz("chars.npz")
+    m, d = chars_inputs(g)
+    out = CL.calc_std_12(d.copy(), m.copy())
+    assert np.array_equal(out["permno"].values, g["std_permno"])
+    assert_series_close(out["rolling_std_252"].values, g["std_rolling_std_252"], "std_12")
+
+
+def _ragged_firm_panel(rng, nfirms, maxlen):
+    lens = rng.integers(1, maxlen + 1, nfirms)
+    lens[::5] = maxlen
+    ids = np.repeat(np.arange(nfirms, dtype=np.int64) * 3 + 10, lens)
+    n = len(ids)
+    f = {k: rng.standard_t(4, n) * 0.1 + (1.0 if k not in ("retx", "accruals", "earnings") else 0.0)
+         for k in CO.FIELDS}
+    for k in ("me", "be", "assets", "shrout", "prc", "total_debt", "sales"):
+        f[k] = np.exp(rng.normal(3, 1, n))
+    for k in CO.FIELDS:
+        f[k][rng.random(n) < 0.02] = np.nan
+    return ids, f
+
+
+def test_firm_chars_vs_oracle_many_tiles(E):
+    """Ragged firms across many 256-row tiles (halo reads across tile and firm edges)."""
+    import torch
+    rng = np.random.default_rng(31)
+    ids, f = _ragged_firm_panel(rng, 900, 130)
+    exp = CO.firm_chars(ids, f)
+    got = E.firm_chars(torch.from_numpy(ids).cuda(), {k: torch.from_numpy(v).cuda() for k, v in f.items()})
+    for col in CO.CHARS:
+        assert_series_close(got[col].cpu().numpy(), exp[col], col)
+    # a subset of characteristics reads only its fields
+    sub = E.firm_chars(torch.from_numpy(ids).cuda(), {"me": torch.from_numpy(f["me"]).cuda()},
+                       names=("log_size",))
+    assert _same(sub["log_size"].cpu().numpy(), got["log_size"].cpu().numpy())
+    with pytest.raises(Exception):
+        E.firm_chars(torch.from_numpy(ids).cuda(), {"me": torch.from_numpy(f["me"]).cuda()},
+                     names=("log_bm",))
+
+
+@pytest.mark.parametrize("window,minp", [(252, 100), (5, 3), (1, 1), (3000, 2)])
+def test_rolling_std_vs_oracle(E, window, minp):
+    import torch
+    rng = np.random.default_rng(window)
+    lens = rng.integers(1, 4000, 40)
+    ids = np.repeat(np.arange(40, dtype=np.int64), lens)
+    x = rng.normal(0, 0.02, len(ids))
+    x[rng.random(len(ids)) < 0.05] = np.nan
+    x[rng.random(len(ids)) < 0.002] = np.inf
+    x[1000:1300] = 0.01                       # a run of equal values -> exact 0
+    exp = CO.rolling_std(ids, x, window, minp, 1.0)
+    got = E.rolling_std(torch.from_numpy(ids).cuda(), torch.from_numpy(x).cuda(), window, minp, 1.0)
+    assert_series_close(got.cpu().numpy(), exp, f"rolling_std w={window}")
+
+
+def test_chars_empty_and_single_row(E):
+    import torch
+    for n in (0, 1):
+        ids = torch.arange(n, dtype=torch.int64, device="cuda")
+        flds = {k: torch.ones(n, dtype=torch.float64, device="cuda") for k in CO.FIELDS}
+        out = E.firm_chars(ids, flds)
+        assert all(v.shape == (n,) for v in out.values())
+        sd = E.rolling_std(ids, flds["retx"], 252, 100)
+        assert sd.shape == (n,) and (n == 0 or torch.isnan(sd).all())
+
+
+def test_firm_chars_full_size_firm_locality(E):
+    """Bench-size firm-major panel (5,000 firms x 600 months): a firm's characteristics depend
+    on its own rows only, so the device result on the whole panel must equal the oracle run on
+    a sample of firms alone."""
+    import torch
+    from fmcore import synth_chars
+    ids_d, flds_d = synth_chars.device_raw_panel(5000, 600, seed=5)
+    got = E.firm_chars(ids_d, flds_d)
+    ids = ids_d.cpu().numpy()
+    pick = np.isin(ids, ids[np.random.default_rng(0).choice(len(ids), 40)])
+    exp = CO.firm_chars(ids[pick], {k: v.cpu().numpy()[pick] for k, v in flds_d.items()})
+    for col in CO.CHARS:
+        assert_series_close(got[col].cpu().numpy()[pick], exp[col], col)
