@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-months", type=int, default=240, help="oracle CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-chars", action="store_true", help="skip the firm-characteristic stage")
     ap.add_argument("--check", action="store_true", help="verify one step against the oracle")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
     return ap.parse_args()
@@ -232,12 +233,73 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(panel, args, LW)
+    if rank == 0 and world == 1 and not args.no_chars:
+        result["firm_chars"] = firm_chars_stage(args, E)
     if args.check and rank == 0 and world == 1:
         result["check"] = check_against_oracle(panel, gres, summ, args, LW)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def firm_chars_stage(args, E):
+    """SURVEY.md §8(f) row 2, measured beside the headline (not part of `value`): the twelve
+    get_factors characteristics (fm_firm_chars) on a firm-major 5,000-firm x 600-month panel
+    and calc_std_12's rolling std (fm_rolling_std) on 5,000 firms x 2,520 trading days, both
+    resident in HBM; device time = the launch re-issued back to back (HIP events on the
+    launch stream).  Algorithmic bytes: 12 fields + id read, 12 outputs written = 200 B per
+    monthly row; id + retx read, std written = 24 B per daily row."""
+    from fmcore import synth_chars
+    res = {}
+    ids, flds = synth_chars.device_raw_panel(args.firms, 600, seed=args.seed)
+    E.firm_chars(ids, flds)
+    torch.cuda.synchronize()
+    ms = E.time_launch("fm_firm_chars", 20)
+    rows = int(ids.shape[0])
+    gbs = rows * 200 / (ms * 1e-3) / 1e9
+    res["monthly"] = {"rows": rows, "ms": ms, "rows_per_s": rows / (ms * 1e-3),
+                      "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": rows * 200}}
+    del flds
+    dids, x = synth_chars.device_daily_returns(args.firms, 2520, seed=args.seed)
+    out = torch.empty_like(x)
+    E.rolling_std(dids, x, out=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        E.rolling_std(dids, x, out=out)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    drows = int(x.shape[0])
+    gbs = drows * 24 / (ms * 1e-3) / 1e9
+    res["daily_std"] = {"rows": drows, "ms": ms, "rows_per_s": drows / (ms * 1e-3),
+                        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": drows * 24}}
+    if not args.no_cpu:
+        from oracle import chars_oracle as CO
+        nf = 200
+        ids2, fl2 = synth_chars.device_raw_panel(nf, 600, seed=args.seed + 1)
+        fh = {k: v.cpu().numpy() for k, v in fl2.items()}
+        ih = ids2.cpu().numpy()
+        t0 = time.perf_counter()
+        CO.firm_chars(ih, fh)
+        dt = time.perf_counter() - t0
+        res["monthly"]["cpu_baseline"] = {"value": len(ih) / dt, "unit": "firm-month rows/s", "cores": 1,
+                                          "kind": "port", "sample": f"{nf} firms x 600 months, "
+                                          "oracle/chars_oracle.py firm_chars (vectorized numpy)"}
+        nd = 20
+        di, dx = synth_chars.device_daily_returns(nd, 2520, seed=args.seed + 1)
+        di, dx = di.cpu().numpy(), dx.cpu().numpy()
+        t0 = time.perf_counter()
+        CO.rolling_std(di, dx)
+        dt = time.perf_counter() - t0
+        res["daily_std"]["cpu_baseline"] = {"value": len(dx) / dt, "unit": "firm-day rows/s", "cores": 1,
+                                            "kind": "port", "sample": f"{nd} firms x 2520 days, "
+                                            "oracle/chars_oracle.py rolling_std (per-row window)"}
+    return res
 
 
 def cpu_baseline(panel, args, LW):

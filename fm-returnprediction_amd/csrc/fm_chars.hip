@@ -10,9 +10,9 @@
 //                         are coalesced global loads that hit L2 (the previous tile's rows).
 //                         Because groups are contiguous, "row i-k belongs to row i's firm" is
 //                         one compare: ids[i-k] == ids[i].
-//   rolling_std_kernel <- calc_std_12's 252-day rolling std (:448-456): each thread owns 8
-//                         consecutive rows; the first window is summed directly (two-pass
-//                         from LDS), the next 7 slide by Welford remove/add.  pandas slides
+//   rolling_std_kernel <- calc_std_12's 252-day rolling std (:448-456): each thread owns 16
+//                         consecutive rows; the first window is summed directly (one pass
+//                         of shifted sums from LDS), the next 15 slide by Welford remove/add.  pandas slides
 //                         one Welford/Kahan state along the whole group; both agree to
 //                         rounding (tests: 1e-9 series-RMS tolerance).
 #include <math.h>
@@ -34,87 +34,109 @@ __global__ __launch_bounds__(CT) void firm_chars_kernel(fm_chars_args a, int nee
     __shared__ double dv[CT + CH];    // dvc, +-inf -> NaN (:273-278)
     const int64_t n = a.n;
     const int64_t b = (int64_t)blockIdx.x * CT;
+    const int64_t i = b + threadIdx.x;
+    const bool live = i < n;
+    const int64_t ic = live ? i : n - 1;   // clamped row: every load below is unconditional
+    double* const* o = a.out;
+    // ---- this row's global loads, issued before the tile barrier so they fly while the
+    // halo is staged (each a coalesced read; lags hit L2: the previous rows of this tile or
+    // the previous tile).  Pointer tests are kernel-argument (scalar) branches.
+    auto ld = [&](int f, int k) {
+        const double* p = a.field[f];
+        return p[ic - k >= 0 ? ic - k : 0];
+    };
+    const bool need_me1 = o[FM_CHAR_LOG_SIZE] || o[FM_CHAR_LOG_BM] || o[FM_CHAR_DEBT_PRICE] ||
+                          o[FM_CHAR_SALES_PRICE];
+    const bool need_sh = o[FM_CHAR_LOG_ISSUES_12] || o[FM_CHAR_LOG_ISSUES_36];
+    const double me1 = need_me1 ? ld(FM_FIELD_ME, 1) : 0.0;
+    const double be1 = o[FM_CHAR_LOG_BM] ? ld(FM_FIELD_BE, 1) : 0.0;
+    const double acc = o[FM_CHAR_ACCRUALS_FINAL] ? ld(FM_FIELD_ACCRUALS, 0) : 0.0;
+    const double dep = o[FM_CHAR_ACCRUALS_FINAL] ? ld(FM_FIELD_DEPRECIATION, 0) : 0.0;
+    const double ern = o[FM_CHAR_ROA] ? ld(FM_FIELD_EARNINGS, 0) : 0.0;
+    const bool need_as = o[FM_CHAR_ROA] || o[FM_CHAR_LOG_ASSETS_GROWTH];
+    const double as0 = need_as ? ld(FM_FIELD_ASSETS, 0) : 0.0;
+    const double as12 = o[FM_CHAR_LOG_ASSETS_GROWTH] ? ld(FM_FIELD_ASSETS, 12) : 0.0;
+    const double prc1 = o[FM_CHAR_DY] ? ld(FM_FIELD_PRC, 1) : 0.0;
+    const double sh1 = need_sh ? ld(FM_FIELD_SHROUT, 1) : 0.0;
+    const double sh12 = o[FM_CHAR_LOG_ISSUES_12] ? ld(FM_FIELD_SHROUT, 12) : 0.0;
+    const double sh36 = o[FM_CHAR_LOG_ISSUES_36] ? ld(FM_FIELD_SHROUT, 36) : 0.0;
+    const double td = o[FM_CHAR_DEBT_PRICE] ? ld(FM_FIELD_TOTAL_DEBT, 0) : 0.0;
+    const double sl = o[FM_CHAR_SALES_PRICE] ? ld(FM_FIELD_SALES, 0) : 0.0;
     const double* retx = a.field[FM_FIELD_RETX];
     const double* dvc = a.field[FM_FIELD_DVC];
     for (int j = threadIdx.x; j < CT + CH; j += CT) {
         const int64_t r = b - CH + j;
         const bool in = r >= 0 && r < n;
-        sid[j] = in ? a.ids[r] : 0;
+        const int64_t rc = r < 0 ? 0 : (r < n ? r : n - 1);
+        sid[j] = in ? a.ids[rc] : 0;
         if (need_ret) {
-            const double x = in ? retx[r] : (double)NAN;
-            const double o = 1.0 + x;
-            opr[j] = nan_if_inf(o);
-            lr[j] = nan_if_inf(log(o));
+            const double x = retx[rc];
+            const double op = 1.0 + (in ? x : (double)NAN);
+            opr[j] = nan_if_inf(op);
+            lr[j] = nan_if_inf(log(op));
         }
-        if (need_dvc) dv[j] = in ? nan_if_inf(dvc[r]) : (double)NAN;
+        if (need_dvc) {
+            const double v = dvc[rc];
+            dv[j] = in ? nan_if_inf(v) : (double)NAN;
+        }
     }
     __syncthreads();
-    const int64_t i = b + threadIdx.x;
-    if (i >= n) return;
+    if (!live) return;
     const int li = threadIdx.x + CH;
     const int64_t id = sid[li];
     auto same = [&](int k) { return i - k >= 0 && sid[li - k] == id; };
-    // lag-k value of a field (NaN outside the firm); the load is clamped, not branched
-    auto lag = [&](int f, int k) {
-        const double* p = a.field[f];
-        const double v = p[i - k >= 0 ? i - k : 0];
-        return same(k) ? v : (double)NAN;
-    };
-    double* const* o = a.out;
-    const bool need_me1 = o[FM_CHAR_LOG_SIZE] || o[FM_CHAR_LOG_BM] || o[FM_CHAR_DEBT_PRICE] ||
-                          o[FM_CHAR_SALES_PRICE];
-    const double me1 = need_me1 ? lag(FM_FIELD_ME, 1) : 0.0;
-    if (o[FM_CHAR_LOG_SIZE]) o[FM_CHAR_LOG_SIZE][i] = log(me1);
-    if (o[FM_CHAR_LOG_BM]) o[FM_CHAR_LOG_BM][i] = log(lag(FM_FIELD_BE, 1)) - log(me1);
+    const double nan = NAN;
+    const double m1 = same(1) ? me1 : nan;
+    if (o[FM_CHAR_LOG_SIZE]) o[FM_CHAR_LOG_SIZE][i] = log(m1);
+    if (o[FM_CHAR_LOG_BM]) o[FM_CHAR_LOG_BM][i] = log(same(1) ? be1 : nan) - log(m1);
     if (o[FM_CHAR_RETURN_12_2]) {
         // rolling(11, min_periods=11).apply(np.prod) of the shift(2) column: rows t-12..t-2,
         // oldest first; any NaN in the window -> NaN (the product propagates it)
         double p = opr[li - 12];
 #pragma unroll
         for (int k = 11; k >= 2; --k) p *= opr[li - k];
-        o[FM_CHAR_RETURN_12_2][i] = same(12) ? p - 1.0 : (double)NAN;
+        o[FM_CHAR_RETURN_12_2][i] = same(12) ? p - 1.0 : nan;
     }
-    if (o[FM_CHAR_ACCRUALS_FINAL])
-        o[FM_CHAR_ACCRUALS_FINAL][i] = a.field[FM_FIELD_ACCRUALS][i] - a.field[FM_FIELD_DEPRECIATION][i];
-    if (o[FM_CHAR_ROA]) o[FM_CHAR_ROA][i] = a.field[FM_FIELD_EARNINGS][i] / a.field[FM_FIELD_ASSETS][i];
-    if (o[FM_CHAR_LOG_ASSETS_GROWTH])
-        o[FM_CHAR_LOG_ASSETS_GROWTH][i] = log(a.field[FM_FIELD_ASSETS][i] / lag(FM_FIELD_ASSETS, 12));
+    if (o[FM_CHAR_ACCRUALS_FINAL]) o[FM_CHAR_ACCRUALS_FINAL][i] = acc - dep;
+    if (o[FM_CHAR_ROA]) o[FM_CHAR_ROA][i] = ern / as0;
+    if (o[FM_CHAR_LOG_ASSETS_GROWTH]) o[FM_CHAR_LOG_ASSETS_GROWTH][i] = log(as0 / (same(12) ? as12 : nan));
     if (o[FM_CHAR_DY]) {
         // rolling(12, min_periods=1).sum(): the observations among the firm's last 12 rows
-        double s = 0.0;
+        double sum = 0.0;
         int cnt = 0;
 #pragma unroll
         for (int k = 11; k >= 0; --k) {
             const double v = dv[li - k];
             const bool ok = same(k) && !isnan(v);
-            s += ok ? v : 0.0;
+            sum += ok ? v : 0.0;
             cnt += ok ? 1 : 0;
         }
-        o[FM_CHAR_DY][i] = (cnt > 0 ? s : (double)NAN) / lag(FM_FIELD_PRC, 1);
+        o[FM_CHAR_DY][i] = (cnt > 0 ? sum : nan) / (same(1) ? prc1 : nan);
     }
     if (o[FM_CHAR_LOG_RETURN_13_36]) {
         // rolling(24, min_periods=24).sum() of the shift(13) column: all 24 rows t-36..t-13
-        double s = 0.0;
+        double sum = 0.0;
 #pragma unroll
-        for (int k = 36; k >= 13; --k) s += lr[li - k];
-        o[FM_CHAR_LOG_RETURN_13_36][i] = same(36) ? s : (double)NAN;
+        for (int k = 36; k >= 13; --k) sum += lr[li - k];
+        o[FM_CHAR_LOG_RETURN_13_36][i] = same(36) ? sum : nan;
     }
-    if (o[FM_CHAR_LOG_ISSUES_12] || o[FM_CHAR_LOG_ISSUES_36]) {
-        const double l1 = log(lag(FM_FIELD_SHROUT, 1));
-        if (o[FM_CHAR_LOG_ISSUES_12]) o[FM_CHAR_LOG_ISSUES_12][i] = l1 - log(lag(FM_FIELD_SHROUT, 12));
-        if (o[FM_CHAR_LOG_ISSUES_36]) o[FM_CHAR_LOG_ISSUES_36][i] = l1 - log(lag(FM_FIELD_SHROUT, 36));
+    if (need_sh) {
+        const double l1 = log(same(1) ? sh1 : nan);
+        if (o[FM_CHAR_LOG_ISSUES_12]) o[FM_CHAR_LOG_ISSUES_12][i] = l1 - log(same(12) ? sh12 : nan);
+        if (o[FM_CHAR_LOG_ISSUES_36]) o[FM_CHAR_LOG_ISSUES_36][i] = l1 - log(same(36) ? sh36 : nan);
     }
-    if (o[FM_CHAR_DEBT_PRICE]) o[FM_CHAR_DEBT_PRICE][i] = a.field[FM_FIELD_TOTAL_DEBT][i] / me1;
-    if (o[FM_CHAR_SALES_PRICE]) o[FM_CHAR_SALES_PRICE][i] = a.field[FM_FIELD_SALES][i] / me1;
+    if (o[FM_CHAR_DEBT_PRICE]) o[FM_CHAR_DEBT_PRICE][i] = td / m1;
+    if (o[FM_CHAR_SALES_PRICE]) o[FM_CHAR_SALES_PRICE][i] = sl / m1;
 }
 
 // ---- rolling std --------------------------------------------------------------------------
 constexpr int ST_T = 256;            // threads
-constexpr int ST_R = 8;              // consecutive rows per thread
+constexpr int ST_R = 16;             // consecutive rows per thread
 constexpr int ST_ROWS = ST_T * ST_R; // rows per tile
 
-// LDS slot of halo element e: one pad slot per 8 (lanes 8 rows apart hit distinct banks)
-__host__ __device__ __forceinline__ int spad(int e) { return e + (e >> 3); }
+// LDS slot of halo element e: one pad slot per ST_R (the lanes of a wave read elements
+// ST_R apart; stride ST_R + 1 doubles puts 32 lanes on distinct bank pairs)
+__host__ __device__ __forceinline__ int spad(int e) { return e + e / ST_R; }
 
 __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __restrict__ ids,
                                                            const double* __restrict__ x, int64_t n,
@@ -129,32 +151,81 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     for (int e = threadIdx.x; e < E; e += ST_T) {
         const int64_t r = b - H + e;
         const bool in = r >= 0 && r < n;
-        xs[spad(e)] = in ? nan_if_inf(x[r]) : (double)NAN;
-        is[spad(e)] = in ? ids[r] : 0;
+        const int64_t rc = r < 0 ? 0 : (r < n ? r : n - 1);
+        const double v = x[rc];
+        const int64_t id = ids[rc];
+        xs[spad(e)] = in ? nan_if_inf(v) : (double)NAN;
+        is[spad(e)] = in ? id : 0;
     }
     __syncthreads();
     const int e0 = H + threadIdx.x * ST_R;   // halo index of this thread's first row
     const int64_t i0 = b + threadIdx.x * ST_R;
     if (i0 >= n) return;
     const int64_t id0 = is[spad(e0)];
-    // first window: rows max(i0 - H, firm start)..i0, direct two-pass
-    const int lo = (int)(i0 - H >= 0 ? e0 - H : e0 - i0);
-    int cnt = 0, run = 0;
-    double sum = 0.0, last = NAN;
-    for (int e = lo; e <= e0; ++e) {
-        const double v = xs[spad(e)];
-        if (is[spad(e)] != id0 || isnan(v)) continue;
-        ++cnt;
-        sum += v;
-        run = v == last ? run + 1 : 1;
-        last = v;
+    // first window: halo rows [lo, e0], lo = max(e0 - H, row 0, the firm's first row).  The
+    // firm's rows are contiguous, so "row e belongs to the firm" is monotone over [lo, e0]:
+    // binary search for its first true.
+    int lo = (int)(i0 - H >= 0 ? e0 - H : e0 - i0);
+    {
+        int hi = e0;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (is[spad(mid)] == id0) hi = mid;
+            else lo = mid + 1;
+        }
     }
-    double mean = cnt > 0 ? sum / (double)cnt : 0.0, m2 = 0.0;
-    for (int e = lo; e <= e0; ++e) {
+    // one pass, four independent chains: count, sums of (x - K) and (x - K)^2 with K = an
+    // observation near the window end (a data value, so the shifted second moment loses no
+    // precision), min and max (all observations equal <=> pandas' consecutive-same-value rule)
+    double K = 0.0;
+    for (int e = e0; e >= lo && e > e0 - 8; --e) {
         const double v = xs[spad(e)];
-        if (is[spad(e)] != id0 || isnan(v)) continue;
-        const double d = v - mean;
-        m2 += d * d;
+        if (!isnan(v)) {
+            K = v;
+            break;
+        }
+    }
+    int c4[4] = {0, 0, 0, 0};
+    double a4[4] = {0.0, 0.0, 0.0, 0.0}, q4[4] = {0.0, 0.0, 0.0, 0.0};
+    double mn4[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+    double mx4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    auto take = [&](int j, double v) {
+        const bool ok = !isnan(v);
+        const double d = ok ? v - K : 0.0;
+        a4[j] += d;
+        q4[j] += d * d;
+        c4[j] += ok ? 1 : 0;
+        mn4[j] = fmin(mn4[j], v);
+        mx4[j] = fmax(mx4[j], v);
+    };
+    int e = lo;
+    for (; e + 3 <= e0; e += 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) take(j, xs[spad(e + j)]);
+    }
+    for (int j = 0; e <= e0; ++e, ++j) take(j, xs[spad(e)]);
+    int cnt = c4[0] + c4[1] + c4[2] + c4[3];
+    const double s1 = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    const double s2 = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+    const double mn = fmin(fmin(mn4[0], mn4[1]), fmin(mn4[2], mn4[3]));
+    const double mx = fmax(fmax(mx4[0], mx4[1]), fmax(mx4[2], mx4[3]));
+    double mean = cnt > 0 ? K + s1 / (double)cnt : 0.0;
+    double m2 = cnt > 0 ? s2 - s1 * (s1 / (double)cnt) : 0.0;
+    // trailing run of equal observations (sliding below needs it): the whole count when all
+    // are equal, else counted back from the window end to the first different observation
+    int run = 0;
+    double last = NAN;
+    if (cnt > 0 && mn == mx) {
+        run = cnt;
+        last = mn;
+    } else {
+        for (int f = e0; f >= lo; --f) {
+            const double v = xs[spad(f)];
+            if (isnan(v)) continue;
+            if (run > 0 && v != last) break;
+            last = v;
+            ++run;
+        }
     }
     const int need = minp > 2 ? minp : 2;
     for (int r = 0; r < ST_R; ++r) {
