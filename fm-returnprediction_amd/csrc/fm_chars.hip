@@ -11,8 +11,9 @@
 //                         Because groups are contiguous, "row i-k belongs to row i's firm" is
 //                         one compare: ids[i-k] == ids[i].
 //   rolling_std_kernel <- calc_std_12's 252-day rolling std (:448-456): each thread owns 16
-//                         consecutive rows; the first window is summed directly (one pass
-//                         of shifted sums from LDS), the next 15 slide by Welford remove/add.  pandas slides
+//                         consecutive rows; the first window merges per-16-row block states
+//                         (count, mean, M2; Chan et al.) precomputed in LDS for the tile and
+//                         its halo, the next 15 slide by Welford remove/add.  pandas slides
 //                         one Welford/Kahan state along the whole group; both agree to
 //                         rounding (tests: 1e-9 series-RMS tolerance).
 #include <math.h>
@@ -133,10 +134,48 @@ __global__ __launch_bounds__(CT) void firm_chars_kernel(fm_chars_args a, int nee
 constexpr int ST_T = 256;            // threads
 constexpr int ST_R = 16;             // consecutive rows per thread
 constexpr int ST_ROWS = ST_T * ST_R; // rows per tile
+constexpr int ST_LU = 9;             // tile-load batch per thread (4096 + 251 halo rows = 17 per thread)
 
 // LDS slot of halo element e: one pad slot per ST_R (the lanes of a wave read elements
 // ST_R apart; stride ST_R + 1 doubles puts 32 lanes on distinct bank pairs)
 __host__ __device__ __forceinline__ int spad(int e) { return e + e / ST_R; }
+
+// count / mean / M2 of the non-NaN observations of halo rows [a, b): two passes, no division
+// per observation
+struct RunStats {
+    int n;
+    double mean;
+    double m2;
+};
+
+__device__ __forceinline__ RunStats range_stats(const double* xs, int a, int b) {
+    int c = 0;
+    double s1 = 0.0;
+    for (int e = a; e < b; ++e) {
+        const double v = xs[spad(e)];
+        const bool ok = !isnan(v);
+        s1 += ok ? v : 0.0;
+        c += ok ? 1 : 0;
+    }
+    const double mean = c > 0 ? s1 / (double)c : 0.0;
+    double m2 = 0.0;
+    for (int e = a; e < b; ++e) {
+        const double v = xs[spad(e)];
+        const double d = isnan(v) ? 0.0 : v - mean;
+        m2 += d * d;
+    }
+    return RunStats{c, mean, m2};
+}
+
+// pairwise merge of two states (Chan, Golub & LeVeque)
+__device__ __forceinline__ RunStats merge_stats(RunStats a, RunStats b) {
+    if (b.n == 0) return a;
+    if (a.n == 0) return b;
+    const int nn = a.n + b.n;
+    const double d = b.mean - a.mean;
+    const double f = (double)b.n / (double)nn;
+    return RunStats{nn, a.mean + d * f, a.m2 + b.m2 + d * d * (double)a.n * f};
+}
 
 __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __restrict__ ids,
                                                            const double* __restrict__ x, int64_t n,
@@ -148,18 +187,48 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     double* xs = sm;
     int64_t* is = (int64_t*)(sm + spad(E) + 1);
     const int64_t b = (int64_t)blockIdx.x * ST_ROWS;
-    for (int e = threadIdx.x; e < E; e += ST_T) {
-        const int64_t r = b - H + e;
-        const bool in = r >= 0 && r < n;
-        const int64_t rc = r < 0 ? 0 : (r < n ? r : n - 1);
-        const double v = x[rc];
-        const int64_t id = ids[rc];
-        xs[spad(e)] = in ? nan_if_inf(v) : (double)NAN;
-        is[spad(e)] = in ? id : 0;
+    // ST_LU rows per thread in flight: all loads of a batch are issued (clamped, so always
+    // in bounds) before the first LDS store waits on them
+    for (int e1 = threadIdx.x; e1 < E; e1 += ST_T * ST_LU) {
+        double v[ST_LU];
+        int64_t id[ST_LU];
+#pragma unroll
+        for (int k = 0; k < ST_LU; ++k) {
+            const int64_t r = b - H + e1 + k * ST_T;
+            const int64_t rc = r < 0 ? 0 : (r < n ? r : n - 1);
+            v[k] = x[rc];
+            id[k] = ids[rc];
+        }
+#pragma unroll
+        for (int k = 0; k < ST_LU; ++k) {
+            const int e = e1 + k * ST_T;
+            const int64_t r = b - H + e;
+            const bool in = r >= 0 && r < n;
+            if (e < E) {
+                xs[spad(e)] = in ? nan_if_inf(v[k]) : (double)NAN;
+                is[spad(e)] = in ? id[k] : 0;
+            }
+        }
     }
     __syncthreads();
-    const int e0 = H + threadIdx.x * ST_R;   // halo index of this thread's first row
-    const int64_t i0 = b + threadIdx.x * ST_R;
+    // per-16-row block statistics (count, mean, M2 about the block mean; two-pass) for this
+    // tile's own blocks and the nh whole blocks of the halo, so a first window merges ~W/16
+    // block states (Chan et al.) instead of summing W observations
+    const int nh = H / ST_R;
+    const int NB = ST_T + nh;
+    double* bmean = (double*)(is + spad(E) + 1);
+    double* bm2 = bmean + NB;
+    int* bcnt = (int*)(bm2 + NB);
+    for (int s = threadIdx.x; s < NB; s += ST_T) {
+        const RunStats st = range_stats(xs, H + (s - nh) * ST_R, H + (s - nh + 1) * ST_R);
+        bmean[s] = st.mean;
+        bm2[s] = st.m2;
+        bcnt[s] = st.n;
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    const int e0 = H + t * ST_R;   // halo index of this thread's first row
+    const int64_t i0 = b + t * ST_R;
     if (i0 >= n) return;
     const int64_t id0 = is[spad(e0)];
     // first window: halo rows [lo, e0], lo = max(e0 - H, row 0, the firm's first row).  The
@@ -174,58 +243,32 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
             else lo = mid + 1;
         }
     }
-    // one pass, four independent chains: count, sums of (x - K) and (x - K)^2 with K = an
-    // observation near the window end (a data value, so the shifted second moment loses no
-    // precision), min and max (all observations equal <=> pandas' consecutive-same-value rule)
-    double K = 0.0;
-    for (int e = e0; e >= lo && e > e0 - 8; --e) {
-        const double v = xs[spad(e)];
-        if (!isnan(v)) {
-            K = v;
-            break;
+    // [lo, e0] = a head range, whole blocks jlo..t-1 (all rows inside the firm), row e0
+    const int jlo = lo >= H ? (lo - H + ST_R - 1) / ST_R : -((H - lo) / ST_R);
+    RunStats acc;
+    if (jlo >= t) {
+        acc = range_stats(xs, lo, e0 + 1);
+    } else {
+        acc = range_stats(xs, lo, H + jlo * ST_R);
+        for (int j = jlo; j < t; ++j) {
+            const int s = j + nh;
+            acc = merge_stats(acc, RunStats{bcnt[s], bmean[s], bm2[s]});
         }
+        acc = merge_stats(acc, range_stats(xs, e0, e0 + 1));
     }
-    int c4[4] = {0, 0, 0, 0};
-    double a4[4] = {0.0, 0.0, 0.0, 0.0}, q4[4] = {0.0, 0.0, 0.0, 0.0};
-    double mn4[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
-    double mx4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    auto take = [&](int j, double v) {
-        const bool ok = !isnan(v);
-        const double d = ok ? v - K : 0.0;
-        a4[j] += d;
-        q4[j] += d * d;
-        c4[j] += ok ? 1 : 0;
-        mn4[j] = fmin(mn4[j], v);
-        mx4[j] = fmax(mx4[j], v);
-    };
-    int e = lo;
-    for (; e + 3 <= e0; e += 4) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) take(j, xs[spad(e + j)]);
-    }
-    for (int j = 0; e <= e0; ++e, ++j) take(j, xs[spad(e)]);
-    int cnt = c4[0] + c4[1] + c4[2] + c4[3];
-    const double s1 = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-    const double s2 = (q4[0] + q4[1]) + (q4[2] + q4[3]);
-    const double mn = fmin(fmin(mn4[0], mn4[1]), fmin(mn4[2], mn4[3]));
-    const double mx = fmax(fmax(mx4[0], mx4[1]), fmax(mx4[2], mx4[3]));
-    double mean = cnt > 0 ? K + s1 / (double)cnt : 0.0;
-    double m2 = cnt > 0 ? s2 - s1 * (s1 / (double)cnt) : 0.0;
-    // trailing run of equal observations (sliding below needs it): the whole count when all
-    // are equal, else counted back from the window end to the first different observation
+    int cnt = acc.n;
+    double mean = acc.n > 0 ? acc.mean : 0.0;
+    double m2 = acc.n > 0 ? acc.m2 : 0.0;
+    // trailing run of equal observations (pandas' consecutive-same-value rule; sliding below
+    // keeps it): counted back from the window end to the first different observation
     int run = 0;
     double last = NAN;
-    if (cnt > 0 && mn == mx) {
-        run = cnt;
-        last = mn;
-    } else {
-        for (int f = e0; f >= lo; --f) {
-            const double v = xs[spad(f)];
-            if (isnan(v)) continue;
-            if (run > 0 && v != last) break;
-            last = v;
-            ++run;
-        }
+    for (int f = e0; f >= lo; --f) {
+        const double v = xs[spad(f)];
+        if (isnan(v)) continue;
+        if (run > 0 && v != last) break;
+        last = v;
+        ++run;
     }
     const int need = minp > 2 ? minp : 2;
     for (int r = 0; r < ST_R; ++r) {
@@ -327,7 +370,8 @@ extern "C" int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, in
     FM_REQUIRE(window >= 1 && window <= 4096, "fm_rolling_std: window must be 1..4096");
     FM_REQUIRE(min_periods >= 1 && min_periods <= window, "fm_rolling_std: min_periods must be 1..window");
     const int E = ST_ROWS + window - 1;
-    const size_t lds = (size_t)(spad(E) + 1) * 8 * 2;
+    const int nb = ST_T + (window - 1) / ST_R;
+    const size_t lds = (size_t)(spad(E) + 1) * 8 * 2 + (size_t)nb * (8 * 2 + 4);
     FM_REQUIRE(lds <= 160 * 1024, "fm_rolling_std: window too large for LDS");
     const int64_t blocks = (n + ST_ROWS - 1) / ST_ROWS;
     FM_REQUIRE(blocks < (1ll << 31), "fm_rolling_std: too many rows");
