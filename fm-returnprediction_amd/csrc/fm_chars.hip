@@ -13,7 +13,8 @@
 //   rolling_std_kernel <- calc_std_12's 252-day rolling std (:448-456): each thread owns 16
 //                         consecutive rows; the first window merges per-16-row block states
 //                         (count, mean, M2; Chan et al.) precomputed in LDS for the tile and
-//                         its halo, the next 15 slide by Welford remove/add.  pandas slides
+//                         its halo; the next 15 rows slide shifted sums about the first
+//                         window's mean (adds only, one division per output).  pandas slides
 //                         one Welford/Kahan state along the whole group; both agree to
 //                         rounding (tests: 1e-9 series-RMS tolerance).
 #include <math.h>
@@ -149,19 +150,24 @@ struct RunStats {
 };
 
 __device__ __forceinline__ RunStats range_stats(const double* xs, int a, int b) {
+    // b - a <= ST_R always (a block, a head range or one row): a fixed, unrolled trip count
+    // with masked lanes lets the LDS reads issue together
+    double v[ST_R];
     int c = 0;
     double s1 = 0.0;
-    for (int e = a; e < b; ++e) {
-        const double v = xs[spad(e)];
-        const bool ok = !isnan(v);
-        s1 += ok ? v : 0.0;
+#pragma unroll
+    for (int k = 0; k < ST_R; ++k) {
+        const bool in = a + k < b;
+        v[k] = in ? xs[spad(in ? a + k : a)] : (double)NAN;
+        const bool ok = !isnan(v[k]);
+        s1 += ok ? v[k] : 0.0;
         c += ok ? 1 : 0;
     }
     const double mean = c > 0 ? s1 / (double)c : 0.0;
     double m2 = 0.0;
-    for (int e = a; e < b; ++e) {
-        const double v = xs[spad(e)];
-        const double d = isnan(v) ? 0.0 : v - mean;
+#pragma unroll
+    for (int k = 0; k < ST_R; ++k) {
+        const double d = isnan(v[k]) ? 0.0 : v[k] - mean;
         m2 += d * d;
     }
     return RunStats{c, mean, m2};
@@ -256,9 +262,13 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
         }
         acc = merge_stats(acc, range_stats(xs, e0, e0 + 1));
     }
+    // sliding state: count and sums of (x - K), (x - K)^2 about K = the first window's mean
+    // (re-anchored at the first observation after the window empties), so a slide step is
+    // adds and one FMA, no division
     int cnt = acc.n;
-    double mean = acc.n > 0 ? acc.mean : 0.0;
-    double m2 = acc.n > 0 ? acc.m2 : 0.0;
+    double K = acc.n > 0 ? acc.mean : 0.0;
+    double s1 = 0.0;
+    double s2 = acc.n > 0 ? acc.m2 : 0.0;
     // trailing run of equal observations (pandas' consecutive-same-value rule; sliding below
     // keeps it): counted back from the window end to the first different observation
     int run = 0;
@@ -280,29 +290,29 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
             if (id != is[spad(e - 1)]) {   // a new firm starts here
                 cnt = 0;
                 run = 0;
-                mean = 0.0;
-                m2 = 0.0;
+                s1 = 0.0;
+                s2 = 0.0;
                 last = NAN;
             } else if (i - W >= 0 && is[spad(e - W)] == id) {   // row i - W leaves the window
                 const double v = xs[spad(e - W)];
                 if (!isnan(v)) {
                     --cnt;
+                    const double d = v - K;
+                    s1 -= d;
+                    s2 -= d * d;
                     if (cnt == 0) {
-                        mean = 0.0;
-                        m2 = 0.0;
-                    } else {
-                        const double d = v - mean;
-                        mean -= d / (double)cnt;
-                        m2 -= d * (v - mean);
+                        s1 = 0.0;
+                        s2 = 0.0;
                     }
                 }
             }
             const double v = xs[spad(e)];
             if (!isnan(v)) {
+                if (cnt == 0) K = v;
                 ++cnt;
-                const double d = v - mean;
-                mean += d / (double)cnt;
-                m2 += d * (v - mean);
+                const double d = v - K;
+                s1 += d;
+                s2 += d * d;
                 run = v == last ? run + 1 : 1;
                 last = v;
             }
@@ -312,7 +322,8 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
             if (run >= cnt) {
                 res = 0.0;   // pandas: every observation in the window is the same value
             } else {
-                const double var = m2 / (double)(cnt - 1);
+                const double c = (double)cnt;
+                const double var = (s2 * c - s1 * s1) / (c * (c - 1.0));
                 res = sqrt(var > 0.0 ? var : 0.0) * scale;
             }
         }
