@@ -191,29 +191,33 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     const int H = W - 1;
     const int E = ST_ROWS + H;
     double* xs = sm;
-    int64_t* is = (int64_t*)(sm + spad(E) + 1);
+    // firm starts as a bit per halo row (one wave ballot per 64 rows) instead of an int64 id
+    // per row: 1 KB instead of 37 KB of LDS, so three workgroups share a CU
+    uint64_t* fb = (uint64_t*)(sm + spad(E) + 1);
+    const int nw = (E + 63) / 64;
     const int64_t b = (int64_t)blockIdx.x * ST_ROWS;
     // ST_LU rows per thread in flight: all loads of a batch are issued (clamped, so always
     // in bounds) before the first LDS store waits on them
     for (int e1 = threadIdx.x; e1 < E; e1 += ST_T * ST_LU) {
         double v[ST_LU];
-        int64_t id[ST_LU];
+        int64_t id[ST_LU], idp[ST_LU];
 #pragma unroll
         for (int k = 0; k < ST_LU; ++k) {
             const int64_t r = b - H + e1 + k * ST_T;
             const int64_t rc = r < 0 ? 0 : (r < n ? r : n - 1);
+            const int64_t rp = rc > 0 ? rc - 1 : 0;
             v[k] = x[rc];
             id[k] = ids[rc];
+            idp[k] = ids[rp];
         }
 #pragma unroll
         for (int k = 0; k < ST_LU; ++k) {
-            const int e = e1 + k * ST_T;
+            const int e = e1 + k * ST_T;   // a wave's 64 lanes hold 64 consecutive, 64-aligned rows
             const int64_t r = b - H + e;
             const bool in = r >= 0 && r < n;
-            if (e < E) {
-                xs[spad(e)] = in ? nan_if_inf(v[k]) : (double)NAN;
-                is[spad(e)] = in ? id[k] : 0;
-            }
+            const uint64_t starts = __ballot(in && (r == 0 || id[k] != idp[k]));
+            if (e < E) xs[spad(e)] = in ? nan_if_inf(v[k]) : (double)NAN;
+            if ((threadIdx.x & 63) == 0 && (e >> 6) < nw) fb[e >> 6] = starts;
         }
     }
     __syncthreads();
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     // block states (Chan et al.) instead of summing W observations
     const int nh = H / ST_R;
     const int NB = ST_T + nh;
-    double* bmean = (double*)(is + spad(E) + 1);
+    double* bmean = (double*)(fb + nw);
     double* bm2 = bmean + NB;
     int* bcnt = (int*)(bm2 + NB);
     for (int s = threadIdx.x; s < NB; s += ST_T) {
@@ -236,19 +240,17 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     const int e0 = H + t * ST_R;   // halo index of this thread's first row
     const int64_t i0 = b + t * ST_R;
     if (i0 >= n) return;
-    const int64_t id0 = is[spad(e0)];
-    // first window: halo rows [lo, e0], lo = max(e0 - H, row 0, the firm's first row).  The
-    // firm's rows are contiguous, so "row e belongs to the firm" is monotone over [lo, e0]:
-    // binary search for its first true.
-    int lo = (int)(i0 - H >= 0 ? e0 - H : e0 - i0);
+    // first window: halo rows [lo, e0], lo = max(e0 - H, the firm's first row): the highest
+    // firm-start bit at or below e0 (fs = -1 when the firm starts before the window)
+    const int lo0 = e0 - H;
+    int fs = -1;
     {
-        int hi = e0;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (is[spad(mid)] == id0) hi = mid;
-            else lo = mid + 1;
-        }
+        int w = e0 >> 6;
+        uint64_t m = fb[w] & ((e0 & 63) == 63 ? ~0ull : ((2ull << (e0 & 63)) - 1));
+        while (m == 0 && w > (lo0 >> 6)) m = fb[--w];
+        if (m != 0) fs = w * 64 + 63 - __clzll((long long)m);
     }
+    const int lo = fs > lo0 ? fs : lo0;
     // [lo, e0] = a head range, whole blocks jlo..t-1 (all rows inside the firm), row e0
     const int jlo = lo >= H ? (lo - H + ST_R - 1) / ST_R : -((H - lo) / ST_R);
     RunStats acc;
@@ -286,14 +288,14 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
         if (i >= n) break;
         const int e = e0 + r;
         if (r > 0) {
-            const int64_t id = is[spad(e)];
-            if (id != is[spad(e - 1)]) {   // a new firm starts here
+            if ((fb[e >> 6] >> (e & 63)) & 1ull) {   // a new firm starts here
+                fs = e;
                 cnt = 0;
                 run = 0;
                 s1 = 0.0;
                 s2 = 0.0;
                 last = NAN;
-            } else if (i - W >= 0 && is[spad(e - W)] == id) {   // row i - W leaves the window
+            } else if (fs <= e - W) {   // row e - W (same firm; NaN if before row 0) leaves
                 const double v = xs[spad(e - W)];
                 if (!isnan(v)) {
                     --cnt;
@@ -382,7 +384,7 @@ extern "C" int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, in
     FM_REQUIRE(min_periods >= 1 && min_periods <= window, "fm_rolling_std: min_periods must be 1..window");
     const int E = ST_ROWS + window - 1;
     const int nb = ST_T + (window - 1) / ST_R;
-    const size_t lds = (size_t)(spad(E) + 1) * 8 * 2 + (size_t)nb * (8 * 2 + 4);
+    const size_t lds = (size_t)(spad(E) + 1) * 8 + (size_t)((E + 63) / 64) * 8 + (size_t)nb * (8 * 2 + 4);
     FM_REQUIRE(lds <= 160 * 1024, "fm_rolling_std: window too large for LDS");
     const int64_t blocks = (n + ST_ROWS - 1) / ST_ROWS;
     FM_REQUIRE(blocks < (1ll << 31), "fm_rolling_std: too many rows");
