@@ -11,10 +11,10 @@
 //                         Because groups are contiguous, "row i-k belongs to row i's firm" is
 //                         one compare: ids[i-k] == ids[i].
 //   rolling_std_kernel <- calc_std_12's 252-day rolling std (:448-456): each thread owns 16
-//                         consecutive rows; the first window merges per-16-row block states
-//                         (count, mean, M2; Chan et al.) precomputed in LDS for the tile and
-//                         its halo; the next 15 rows slide shifted sums about the first
-//                         window's mean (adds only, one division per output).  pandas slides
+//                         consecutive rows; the first window sums per-16-row block states
+//                         (count, mean, M2) precomputed in LDS for the tile and its halo, as
+//                         shifted sums about a block mean near the window end; the next 15
+//                         rows slide those sums (adds only, one division per output).  pandas slides
 //                         one Welford/Kahan state along the whole group; both agree to
 //                         rounding (tests: 1e-9 series-RMS tolerance).
 #include <math.h>
@@ -173,16 +173,6 @@ __device__ __forceinline__ RunStats range_stats(const double* xs, int a, int b) 
     return RunStats{c, mean, m2};
 }
 
-// pairwise merge of two states (Chan, Golub & LeVeque)
-__device__ __forceinline__ RunStats merge_stats(RunStats a, RunStats b) {
-    if (b.n == 0) return a;
-    if (a.n == 0) return b;
-    const int nn = a.n + b.n;
-    const double d = b.mean - a.mean;
-    const double f = (double)b.n / (double)nn;
-    return RunStats{nn, a.mean + d * f, a.m2 + b.m2 + d * d * (double)a.n * f};
-}
-
 __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __restrict__ ids,
                                                            const double* __restrict__ x, int64_t n,
                                                            int W, int minp, double scale,
@@ -222,8 +212,8 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     }
     __syncthreads();
     // per-16-row block statistics (count, mean, M2 about the block mean; two-pass) for this
-    // tile's own blocks and the nh whole blocks of the halo, so a first window merges ~W/16
-    // block states (Chan et al.) instead of summing W observations
+    // tile's own blocks and the nh whole blocks of the halo, so a first window adds ~W/16
+    // block states instead of W observations
     const int nh = H / ST_R;
     const int NB = ST_T + nh;
     double* bmean = (double*)(fb + nw);
@@ -253,24 +243,53 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     const int lo = fs > lo0 ? fs : lo0;
     // [lo, e0] = a head range, whole blocks jlo..t-1 (all rows inside the firm), row e0
     const int jlo = lo >= H ? (lo - H + ST_R - 1) / ST_R : -((H - lo) / ST_R);
-    RunStats acc;
-    if (jlo >= t) {
-        acc = range_stats(xs, lo, e0 + 1);
-    } else {
-        acc = range_stats(xs, lo, H + jlo * ST_R);
-        for (int j = jlo; j < t; ++j) {
-            const int s = j + nh;
-            acc = merge_stats(acc, RunStats{bcnt[s], bmean[s], bm2[s]});
-        }
-        acc = merge_stats(acc, range_stats(xs, e0, e0 + 1));
+    // window state as count and sums of (x - K), (x - K)^2 about K = a block mean next to
+    // the window end: each block / range state (n, mean, M2) adds n*d and M2 + n*d^2 with
+    // d = mean - K (exact algebra, no division, four independent chains)
+    double K = 0.0;
+    {
+        const int sk = t - 1 + nh;   // block t-1 (inside the window when jlo < t)
+        const double xe = xs[spad(e0)];
+        K = (jlo < t && bcnt[sk] > 0) ? bmean[sk] : (isnan(xe) ? 0.0 : xe);
     }
-    // sliding state: count and sums of (x - K), (x - K)^2 about K = the first window's mean
-    // (re-anchored at the first observation after the window empties), so a slide step is
-    // adds and one FMA, no division
-    int cnt = acc.n;
-    double K = acc.n > 0 ? acc.mean : 0.0;
-    double s1 = 0.0;
-    double s2 = acc.n > 0 ? acc.m2 : 0.0;
+    int cnt = 0;
+    double s1 = 0.0, s2 = 0.0;
+    auto add_state = [&](const RunStats& st) {
+        const double d = st.mean - K;
+        const double nd = (double)st.n * d;
+        cnt += st.n;
+        s1 += nd;
+        s2 += st.m2 + nd * d;
+    };
+    if (jlo >= t) {
+        add_state(range_stats(xs, lo, e0 + 1));
+    } else {
+        add_state(range_stats(xs, lo, H + jlo * ST_R));
+        int c4[4] = {0, 0, 0, 0};
+        double a4[4] = {0.0, 0.0, 0.0, 0.0}, q4[4] = {0.0, 0.0, 0.0, 0.0};
+        int j = jlo;
+        for (; j + 3 < t; j += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int s = j + u + nh;
+                const double d = bmean[s] - K;
+                const double nd = (double)bcnt[s] * d;
+                c4[u] += bcnt[s];
+                a4[u] += nd;
+                q4[u] += bm2[s] + nd * d;
+            }
+        }
+        for (; j < t; ++j) add_state(RunStats{bcnt[j + nh], bmean[j + nh], bm2[j + nh]});
+        cnt += (c4[0] + c4[1]) + (c4[2] + c4[3]);
+        s1 += (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        s2 += (q4[0] + q4[1]) + (q4[2] + q4[3]);
+        const double xe = xs[spad(e0)];
+        if (!isnan(xe)) add_state(RunStats{1, xe, 0.0});
+    }
+    if (cnt == 0) {
+        s1 = 0.0;
+        s2 = 0.0;
+    }
     // trailing run of equal observations (pandas' consecutive-same-value rule; sliding below
     // keeps it): counted back from the window end to the first different observation
     int run = 0;
