@@ -10,11 +10,12 @@
 //                         are coalesced global loads that hit L2 (the previous tile's rows).
 //                         Because groups are contiguous, "row i-k belongs to row i's firm" is
 //                         one compare: ids[i-k] == ids[i].
-//   rolling_std_kernel <- calc_std_12's 252-day rolling std (:448-456): each thread owns 16
-//                         consecutive rows; the first window sums per-16-row block states
-//                         (count, mean, M2) precomputed in LDS for the tile and its halo, as
-//                         shifted sums about a block mean near the window end; the next 15
-//                         rows slide those sums (adds only, one division per output).  pandas slides
+//   rolling_std_kernel <- calc_std_12's 252-day rolling std (:448-456): each thread owns 8
+//                         consecutive rows of a 2,048-row tile; firm starts are a ballot
+//                         bitmask; the first window sums per-8-row block states (count, mean,
+//                         M2) precomputed in LDS for the tile and its halo, as shifted sums
+//                         about a block mean near the window end; the next 7 rows slide those
+//                         sums (adds only, one division per output).  pandas slides
 //                         one Welford/Kahan state along the whole group; both agree to
 //                         rounding (tests: 1e-9 series-RMS tolerance).
 #include <math.h>
@@ -133,9 +134,9 @@ __global__ __launch_bounds__(CT) void firm_chars_kernel(fm_chars_args a, int nee
 
 // ---- rolling std --------------------------------------------------------------------------
 constexpr int ST_T = 256;            // threads
-constexpr int ST_R = 16;             // consecutive rows per thread
+constexpr int ST_R = 8;              // consecutive rows per thread
 constexpr int ST_ROWS = ST_T * ST_R; // rows per tile
-constexpr int ST_LU = 9;             // tile-load batch per thread (4096 + 251 halo rows = 17 per thread)
+constexpr int ST_LU = 9;             // tile-load batch per thread (2048 + 251 halo rows = 9 per thread)
 
 // LDS slot of halo element e: one pad slot per ST_R (the lanes of a wave read elements
 // ST_R apart; stride ST_R + 1 doubles puts 32 lanes on distinct bank pairs)
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
         }
     }
     __syncthreads();
-    // per-16-row block statistics (count, mean, M2 about the block mean; two-pass) for this
+    // per-ST_R-row block statistics (count, mean, M2 about the block mean; two-pass) for this
     // tile's own blocks and the nh whole blocks of the halo, so a first window adds ~W/16
     // block states instead of W observations
     const int nh = H / ST_R;
