@@ -442,12 +442,15 @@ def test_firm_chars_vs_oracle_many_tiles(E):
                      names=("log_bm",))
 
 
-@pytest.mark.parametrize("window,minp", [(252, 100), (5, 3), (1, 1), (3000, 2)])
+@pytest.mark.parametrize("window,minp", [(252, 100), (5, 3), (1, 1), (3000, 2), (4096, 50), (17, 17)])
 def test_rolling_std_vs_oracle(E, window, minp):
+    """Ragged firms (1..3999 rows) crossing the kernel's 2,048-row tiles; firm ids differ only
+    above bit 32 (the firm-start test compares full int64 ids); window sizes from 1 to the
+    4,096 maximum."""
     import torch
     rng = np.random.default_rng(window)
     lens = rng.integers(1, 4000, 40)
-    ids = np.repeat(np.arange(40, dtype=np.int64), lens)
+    ids = np.repeat(np.arange(40, dtype=np.int64) << 33, lens)
     x = rng.normal(0, 0.02, len(ids))
     x[rng.random(len(ids)) < 0.05] = np.nan
     x[rng.random(len(ids)) < 0.002] = np.inf
