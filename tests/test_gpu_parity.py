@@ -484,3 +484,29 @@ def test_firm_chars_full_size_firm_locality(E):
     exp = CO.firm_chars(ids[pick], {k: v.cpu().numpy()[pick] for k, v in flds_d.items()})
     for col in CO.CHARS:
         assert_series_close(got[col].cpu().numpy()[pick], exp[col], col)
+
+
+def test_panel_from_arrow_matches_frame_path(E):
+    """§8(f) row 3: the Arrow ingest (pinned single copy, device month-major gather) builds a
+    DevicePanel bit-identical to panel_from_arrays on the same DataFrame columns."""
+    import pyarrow as pa
+    from fmcore import ingest
+    rng = np.random.default_rng(8)
+    n = 20000
+    months = pd.date_range("1964-01-31", periods=40, freq="ME")
+    df = pd.DataFrame({"mthcaldt": rng.choice(months, n), "retx": rng.normal(1, 10, n),
+                       "x1": rng.normal(0, 1, n), "me": np.exp(rng.normal(5, 2, n)),
+                       "primaryexch": rng.choice(["N", "Q"], n)})
+    df.loc[rng.random(n) < 0.05, "x1"] = np.nan
+    tab = pa.Table.from_pandas(df, preserve_index=False)
+    got = ingest.panel_from_arrow(tab, ["retx", "x1"], me_col="me", exch_col="primaryexch")
+    exp = E.panel_from_arrays([df["retx"].to_numpy(), df["x1"].to_numpy()], ["retx", "x1"],
+                              df["mthcaldt"].values, me=df["me"].to_numpy(),
+                              nyse=(df["primaryexch"] == "N").to_numpy().astype(np.uint8))
+    assert _same(got.cols.cpu().numpy(), exp.cols.cpu().numpy())
+    assert np.array_equal(got.seg_off_h, exp.seg_off_h)
+    assert _same(got.me.cpu().numpy(), exp.me.cpu().numpy())
+    assert np.array_equal(got.nyse.cpu().numpy(), exp.nyse.cpu().numpy())
+    a1, b1 = E.nyse_breakpoints(got)
+    a2, b2 = E.nyse_breakpoints(exp)
+    assert _same(a1.cpu().numpy(), a2.cpu().numpy()) and _same(b1.cpu().numpy(), b2.cpu().numpy())

@@ -142,3 +142,63 @@ def test_reference_test_file_collects_nothing():
         pytest.skip("reference not mounted")
     tree = ast.parse(open(src).read())
     assert not [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name.startswith("test")]
+
+
+def _arrow_frame(n=3000, seed=3):
+    rng = np.random.default_rng(seed)
+    months = pd.date_range("1964-01-31", periods=12, freq="ME")
+    df = pd.DataFrame({
+        "mthcaldt": rng.choice(months, n),
+        "retx": rng.normal(1, 10, n),
+        "log_size": rng.normal(5, 2, n),
+        "me": np.exp(rng.normal(5, 2, n)),
+        "primaryexch": rng.choice(["N", "Q", "A"], n),
+    })
+    df.loc[rng.random(n) < 0.05, "retx"] = np.nan
+    df.loc[rng.random(n) < 0.02, "mthcaldt"] = pd.NaT
+    df.loc[rng.random(n) < 0.02, "primaryexch"] = None
+    return df
+
+
+def test_arrow_host_columns_match_frame_path():
+    """§8(f) row 3: Arrow ingest yields the arrays, month segments and NYSE mask the pandas
+    path (calc_Lewellen_2014.get_subsets / winsorize -> panel_from_arrays) builds."""
+    import pyarrow as pa
+    from fmcore import engine, ingest
+    df = _arrow_frame()
+    tab = pa.Table.from_pandas(df, preserve_index=False)
+    arrays, labels, me, nyse = ingest.arrow_host_columns(tab, ["retx", "log_size"], me_col="me",
+                                                         exch_col="primaryexch")
+    for a, c in zip(arrays, ["retx", "log_size"]):
+        np.testing.assert_array_equal(a, df[c].to_numpy(dtype=np.float64))
+    np.testing.assert_array_equal(me, df["me"].to_numpy())
+    np.testing.assert_array_equal(nyse, (df["primaryexch"] == "N").to_numpy().astype(np.uint8))
+    _, u1, o1, s1 = engine.month_segments(labels)
+    _, u2, o2, s2 = engine.month_segments(df["mthcaldt"].values)
+    np.testing.assert_array_equal(o1, o2)
+    np.testing.assert_array_equal(s1, s2)
+    assert list(u1) == list(u2)
+
+
+def test_arrow_host_columns_from_parquet(tmp_path):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from fmcore import ingest
+    df = _arrow_frame(500, 4)
+    tab = pa.Table.from_pandas(df, preserve_index=False)
+    p = tmp_path / "panel.parquet"
+    pq.write_table(tab, p, row_group_size=128)      # several chunks per column
+    arrays, labels, me, nyse = ingest.arrow_host_columns(str(p), ["retx"], exch_col="primaryexch")
+    np.testing.assert_array_equal(arrays[0], df["retx"].to_numpy())
+    assert me is None and nyse.dtype == np.uint8 and len(labels) == len(df)
+
+
+def test_month_order_radix_matches_month_segments():
+    from fmcore import engine, ingest
+    df = _arrow_frame(5000, 5)
+    for labels in (df["mthcaldt"].values, np.arange(40000) % 33000):   # int16 and wide paths
+        _, u1, o1, s1 = ingest.month_order(labels)
+        _, u2, o2, s2 = engine.month_segments(labels)
+        np.testing.assert_array_equal(o1, o2)
+        np.testing.assert_array_equal(s1, s2)
+        assert len(u1) == len(u2)
