@@ -153,6 +153,9 @@ def month_segments(labels):
     import pandas as pd
     codes, uniq = pd.factorize(labels, sort=True)
     codes = np.asarray(codes)
+    if len(uniq) < 32767:
+        # numpy sorts 16-bit keys stably by radix (vs a merge sort on int64): ~4x at 3M rows
+        codes = codes.astype(np.int16)
     order = np.argsort(codes, kind="stable")
     order = order[codes[order] >= 0]
     counts = np.bincount(codes[codes >= 0], minlength=len(uniq))

@@ -59,19 +59,8 @@ def _fill(dst: np.ndarray, col) -> None:
 
 
 def month_order(labels):
-    """engine.month_segments with the stable sort as a radix sort: numpy sorts 16-bit
-    integer keys stably by radix, so month codes are narrowed to int16 when T < 32767."""
-    import pandas as pd
-    codes, uniq = pd.factorize(labels, sort=True)
-    codes = np.asarray(codes)
-    if len(uniq) < 32767:
-        codes = codes.astype(np.int16)
-    order = np.argsort(codes, kind="stable")
-    order = order[codes[order] >= 0]
-    counts = np.bincount(codes[codes >= 0], minlength=len(uniq))
-    seg_off = np.zeros(len(uniq) + 1, dtype=np.int64)
-    np.cumsum(counts, out=seg_off[1:])
-    return codes, uniq, order, seg_off
+    """engine.month_segments (its stable sort is a 16-bit radix sort when T < 32767)."""
+    return E.month_segments(labels)
 
 
 def arrow_host_columns(source, value_cols: Sequence[str], date_col: str = "mthcaldt",

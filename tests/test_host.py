@@ -193,12 +193,15 @@ def test_arrow_host_columns_from_parquet(tmp_path):
     assert me is None and nyse.dtype == np.uint8 and len(labels) == len(df)
 
 
-def test_month_order_radix_matches_month_segments():
-    from fmcore import engine, ingest
+def test_month_segments_radix_order_is_stable_order():
+    """engine.month_segments narrows month codes to int16 (numpy's stable radix sort); the
+    order must equal the int64 stable sort of the pandas factorize codes."""
+    from fmcore import engine
     df = _arrow_frame(5000, 5)
     for labels in (df["mthcaldt"].values, np.arange(40000) % 33000):   # int16 and wide paths
-        _, u1, o1, s1 = ingest.month_order(labels)
-        _, u2, o2, s2 = engine.month_segments(labels)
-        np.testing.assert_array_equal(o1, o2)
-        np.testing.assert_array_equal(s1, s2)
-        assert len(u1) == len(u2)
+        codes, uniq = pd.factorize(labels, sort=True)
+        ref = np.argsort(np.asarray(codes, dtype=np.int64), kind="stable")
+        ref = ref[codes[ref] >= 0]
+        _, u1, o1, s1 = engine.month_segments(labels)
+        np.testing.assert_array_equal(o1, ref)
+        assert s1[-1] == len(ref) and len(u1) == len(uniq)
