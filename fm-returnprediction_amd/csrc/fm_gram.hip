@@ -16,9 +16,10 @@
 //      universe level give a bucket id; per bucket one wave ballot gives the bucket's row
 //      count (SGPR) and the lane's rank, so the counting sort needs no LDS counters; each
 //      lane writes its z row to the wave's private LDS tile at (bucket offset + rank);
-//   3. per bucket, v_mfma_f64_16x16x4_f64 with A = B = 4 rows of that bucket (lane l holds
-//      z[row l>>4][col l&15]; rows past the bucket's count read as 0) accumulates Z^T Z in
-//      registers (16x16 FP64 tile = 4 doubles per lane; two tiles wide for > 15 columns).
+//   3. per bucket, v_mfma_f64_4x4x4_4b (__builtin_amdgcn_mfma_f64_4x4x4f64, four 4x4
+//      blocks per instruction) with A = B = 4 rows of that bucket accumulates Z^T Z in
+//      registers: three instructions per 4-row group cover the 16x16 Gram (block pairs, see
+//      BlockPairs below; rows past the bucket's count read the zero rows).
 // At chunk end the four waves' accumulators are summed through LDS and written as one
 // packed upper-triangular Gram per (chunk, bucket).  fm_solve combines buckets into
 // problems: model m's Gram is the sum over patterns that contain m and levels >= the

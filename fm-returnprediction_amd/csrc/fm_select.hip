@@ -897,13 +897,12 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
         else launch_select_wave<96>(a, st);
         FM_CHECK_LAUNCH("fm_select_cuts(wave)");
     }
-    // diagnostic only (tools/select_marks.py): FM_SELECT_NO_FALLBACK=1 leaves the wave
-    // kernel's fallback marks (nvalid == -1) in place; results are then incomplete
-    static const bool no_fb = [] {
-        const char* e = getenv("FM_SELECT_NO_FALLBACK");
-        return e != nullptr && e[0] == '1';
-    }();
-    if (wave && no_fb) return FM_OK;
+#ifdef FM_SELECT_DIAG_NO_FALLBACK
+    // diagnostic builds only (-DFM_SELECT_DIAG_NO_FALLBACK, tools/select_marks.py): leave the
+    // wave kernel's fallback marks (nvalid == -1) in place; results are then incomplete.
+    // The shipped library is never built with it.
+    if (wave) return FM_OK;
+#endif
     if (vpt <= 2) launch_select<2>(a, ncols, st, wave);
     else if (vpt <= 4) launch_select<4>(a, ncols, st, wave);
     else if (vpt <= 8) launch_select<8>(a, ncols, st, wave);

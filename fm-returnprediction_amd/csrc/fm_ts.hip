@@ -8,7 +8,8 @@
 //                   weights 1-k/T that stop at the first negative weight (:78-100),
 //                   t = mean/se (:125); also used for mean_R2 / mean_N (:128-129)
 //   fm_rolling_mean rolling(window, min_periods).mean() over the fitted-month rows, NaN
-//                   values skipped and not counted (src/calc_Lewellen_2014.py:926)
+//                   and +-inf values skipped and not counted (pandas' rolling turns inf
+//                   into NaN before its window sums; src/calc_Lewellen_2014.py:926)
 //   fm_predictive   build-defined A7/A8: with c = the rolling coefficients `lag` rows
 //                   earlier, F_i = c0 + c'x_i; the per-month OLS of y on [1, F] has
 //                   slope = c'Sxy / c'Sxx c and R^2 = (c'Sxy)^2 / (c'Sxx c * Syy), both
@@ -121,6 +122,10 @@ __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t 
     const int p = blockIdx.y / kmax, k = blockIdx.y - (blockIdx.y / kmax) * kmax;
     const int c0 = blockIdx.x * RCH;
     const int cnt = count[p];
+    // rows past the fitted-month count have no month: NaN (never left uninitialised)
+    const int cend = c0 + RCH < nseg ? c0 + RCH : nseg;
+    for (int i = (c0 > cnt ? c0 : cnt) + threadIdx.x; i < cend; i += TT)
+        out[((int64_t)p * nseg + i) * kmax + k] = NAN;
     if (c0 >= cnt) return;
     const int32_t* ix = idx + (int64_t)p * nseg;
     const int lo = c0 - window + 1 < 0 ? 0 : c0 - window + 1;
@@ -134,7 +139,7 @@ __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t 
         int c = 0;
         for (int j = j0; j <= i; ++j) {
             const double x = xs[j - lo];
-            if (!isnan(x)) {
+            if (isfinite(x)) {   // pandas rolling: +-inf -> NaN (Window._prep_values)
                 sm += x;
                 ++c;
             }
@@ -419,10 +424,23 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
                               double* lds_d) {
     const int tid = threadIdx.x;
     const int r0 = chunk * RROWS;
-    if (r0 >= cnt) return;                               // block-uniform
-    const int r1 = r0 + RROWS < cnt ? r0 + RROWS : cnt;
     const int T = a.nseg, PM = a.pmax;
     const bool predictive = a.pred != nullptr;
+    {
+        // rows of this chunk past the fitted-month count hold no month: NaN rolling means,
+        // NaN predictive record, status 0 (the buffers are never left uninitialised)
+        const int e0 = r0 > cnt ? r0 : cnt, e1 = r0 + RROWS < T ? r0 + RROWS : T;
+        for (int e = tid; e < (e1 - e0) * PM; e += FT) a.roll[((int64_t)p * T + e0) * PM + e] = NAN;
+        if (predictive)
+            for (int i = e0 + tid; i < e1; i += FT) {
+                double* o = a.pred + ((int64_t)p * T + i) * 4;
+                o[0] = o[1] = o[2] = NAN;
+                o[3] = 0.0;
+                a.pred_status[(int64_t)p * T + i] = 0;
+            }
+    }
+    if (r0 >= cnt) return;                               // block-uniform
+    const int r1 = r0 + RROWS < cnt ? r0 + RROWS : cnt;
     const int q0 = predictive ? (r0 - a.lag > 0 ? r0 - a.lag : 0) : r0;   // rows rolled here
     const int j0 = q0 - a.window + 1 > 0 ? q0 - a.window + 1 : 0;          // rows read
     const int nsrc = r1 - j0, nq = r1 - q0;
@@ -442,7 +460,7 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
         int c = 0;
         for (int j = (i0 - a.window + 1 > 0 ? i0 - a.window + 1 : 0); j <= i0; ++j) {
             const double x = xs[(j - j0) * PM + k];
-            if (!isnan(x)) {
+            if (isfinite(x)) {
                 sm += x;
                 ++c;
             }
@@ -450,14 +468,14 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
         for (int i = i0; i < i1; ++i) {
             if (i > i0) {
                 const double x = xs[(i - j0) * PM + k];
-                if (!isnan(x)) {
+                if (isfinite(x)) {
                     sm += x;
                     ++c;
                 }
                 const int jo = i - a.window;
                 if (jo >= 0) {
                     const double y = xs[(jo - j0) * PM + k];
-                    if (!isnan(y)) {
+                    if (isfinite(y)) {
                         sm -= y;
                         --c;
                     }

@@ -547,6 +547,20 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
                     mom_stride=mom_stride)
 
 
+def drop_degenerate_months(res: FMResult, models: Sequence[Model], sd):
+    """Standardized passes (A9): a month in which a regressor has fewer than two values or
+    zero dispersion has an all-NaN z-score column, so every row drops out and the month is
+    not fitted for the models using it; clear FM_ST_FITTED there.  ``sd`` [C, T]."""
+    bad = ~(sd > 0)                                              # NaN sd -> True
+    C = sd.shape[0]
+    use = np.zeros((res.nprob, C), dtype=np.float64)
+    for k, p in enumerate(res.problems):
+        use[k, models[p.model].xs] = 1.0
+    hit = _small_tensor(tuple(map(tuple, use)), torch.float64, sd.device) @ bad.to(torch.float64)
+    res.status &= ~((hit.t() > 0).to(torch.int32) * L.FM_ST_FITTED)
+    return res
+
+
 # ------------------------------------------------------------------------------------------
 # Time-series stage
 # ------------------------------------------------------------------------------------------
@@ -751,6 +765,12 @@ CHAR_NAMES = ("log_size", "log_bm", "return_12_2", "accruals_final", "roa", "log
               "dy", "log_return_13_36", "log_issues_12", "log_issues_36", "debt_price", "sales_price")
 
 
+def _check_ids(ids):
+    """Firm ids are read as raw int64 words: reject any other dtype / layout."""
+    if ids.dtype != torch.int64 or ids.dim() != 1 or not ids.is_contiguous():
+        raise ValueError("firm ids must be a contiguous int64 [n] tensor")
+
+
 def firm_chars(ids, fields, names=CHAR_NAMES, out=None):
     """Monthly characteristics for FIRM-major rows (each firm's rows contiguous, in frame
     order).  ``ids`` int64 [n]; ``fields`` maps CHAR_FIELDS names -> float64 [n] device
@@ -758,8 +778,11 @@ def firm_chars(ids, fields, names=CHAR_NAMES, out=None):
     ``out`` (optional) is a [len(names), n] float64 tensor to write into."""
     n = int(ids.shape[0])
     dev = ids.device
+    _check_ids(ids)
     if out is None:
         out = torch.empty((len(names), n), dtype=torch.float64, device=dev)
+    if out.dtype != torch.float64 or out.dim() != 2 or out.shape != (len(names), n) or out.stride(1) != 1:
+        raise ValueError("firm_chars: out must be float64 [len(names), n] with contiguous rows")
     a = L.CharsArgs()
     a.ids = ids.data_ptr()
     a.n = n
@@ -767,6 +790,8 @@ def firm_chars(ids, fields, names=CHAR_NAMES, out=None):
     for f, nm in enumerate(CHAR_FIELDS):
         t = fields.get(nm)
         if t is not None:
+            if t.dtype != torch.float64 or t.dim() != 1 or t.shape[0] != n or t.device != dev:
+                raise ValueError(f"firm_chars: field {nm!r} must be a float64 [{n}] tensor on {dev}")
             t = t.contiguous()
             keep.append(t)
             a.field[f] = t.data_ptr()
@@ -780,8 +805,14 @@ def firm_chars(ids, fields, names=CHAR_NAMES, out=None):
 def rolling_std(ids, x, window=252, min_periods=100, scale=252 ** 0.5, out=None):
     """Per-row rolling std (ddof=1) over the last ``window`` rows of each firm group."""
     n = int(x.shape[0])
+    _check_ids(ids)
+    if x.dtype != torch.float64 or x.dim() != 1 or ids.shape[0] != n or x.device != ids.device:
+        raise ValueError("rolling_std: x must be a float64 [n] tensor beside int64 [n] ids")
+    x = x.contiguous()
     if out is None:
         out = torch.empty(n, dtype=torch.float64, device=x.device)
+    if out.dtype != torch.float64 or out.shape != (n,) or not out.is_contiguous():
+        raise ValueError("rolling_std: out must be a contiguous float64 [n] tensor")
     _kcall("fm_rolling_std", "fm_rolling_std", ids.data_ptr(), x.data_ptr(), n, int(window),
            int(min_periods), float(scale), out.data_ptr(), _stream())
     return out

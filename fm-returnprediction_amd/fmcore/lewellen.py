@@ -115,6 +115,20 @@ def _side_stream(device):
     return s
 
 
+def _standardize_params(panel: E.DevicePanel, cuts: E.Cuts, yi: int):
+    """A9 (build-defined): the Gram sees z = (clip(x) - mean_t) / sd_t for every predictor
+    column (shift = mean, inv_scale = 1/sd, nothing added back: the regressors ARE the
+    z-scores), while the dependent column keeps its units (shift = its pivot, scale 1,
+    added back to the intercept).  All [C, T] month tables, built on the device."""
+    shift = cuts.mean.clone()
+    inv_scale = 1.0 / cuts.sd
+    add_back = torch.zeros_like(shift)
+    shift[yi] = cuts.center[yi]
+    inv_scale[yi] = 1.0
+    add_back[yi] = cuts.center[yi]
+    return shift, inv_scale, add_back
+
+
 def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx"):
     """Panel-sized work for one shard of months: cuts, universes, batched Gram + solve."""
     cuts = None
@@ -137,26 +151,27 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
             t.record_stream(main)
         nlevels = 3
         bp = (a, b)
+    add_back = None
     if cfg.winsorize or cfg.standardize:
         mc = 5 if cfg.winsorize else 2 ** 31 - 1
         # standardize needs the exact clipped moments; otherwise the Gram pivot is the
         # select kernel's free center (midpoint of the cuts), and no moments pass runs
         cuts = E.select_cuts(panel, cfg.lower_percentile / 100, cfg.upper_percentile / 100, mc,
-                             E.LERP_NUMPY, moments=cfg.standardize, center=not cfg.standardize)
+                             E.LERP_NUMPY, moments=cfg.standardize, center=True)
+        shift = cuts.center
         if cfg.standardize:
-            shift = torch.where(torch.isfinite(cuts.mean), cuts.mean, E.pilot_shift(panel))
-            inv_scale = 1.0 / cuts.sd
-        else:
-            shift = cuts.center
+            shift, inv_scale, add_back = _standardize_params(panel, cuts, panel.col(y))
         if not cfg.winsorize:
             cuts = E.Cuts(torch.full_like(cuts.lo, float("nan")), torch.full_like(cuts.hi, float("nan")),
-                          cuts.nvalid, cuts.mean, cuts.sd)
+                          cuts.nvalid, cuts.mean, cuts.sd, cuts.center)
     if side is not None:
         main.wait_stream(side)
     models, names = build_models(panel, model_cols, y=y, fig1=cfg.fig1, universes=cfg.universes)
     res = E.fm_pass(panel, models, level=level, nlevels=nlevels, cuts=cuts, shift=shift,
-                    inv_scale=inv_scale, add_back=None if cfg.standardize else shift,
+                    inv_scale=inv_scale, add_back=add_back if cfg.standardize else shift,
                     moments=cfg.forecasts)
+    if cfg.standardize:
+        E.drop_degenerate_months(res, models, cuts.sd)
     return res, names, cuts, level, bp
 
 

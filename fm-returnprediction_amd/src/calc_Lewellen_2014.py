@@ -141,8 +141,18 @@ def standardize(crsp_comp: pd.DataFrame, varlist: list, date_col: str = "mthcald
 # ------------------------------------------------------------------------------------------
 def _firm_grouping(permno):
     """groupby("permno") row order: each firm's rows contiguous, frame order inside a firm
-    (a stable sort by permno; None when the frame is already grouped that way)."""
-    ids = np.asarray(permno, dtype=np.int64)
+    (a stable sort by permno; None when the frame is already grouped that way).  pandas'
+    groupby drops rows whose permno is missing; such rows are rejected here rather than
+    read as a garbage id."""
+    p = np.asarray(permno)
+    if p.dtype.kind == "f":
+        if np.isnan(p).any():
+            raise ValueError("permno contains NaN: drop those rows first (groupby would drop them)")
+    elif p.dtype.kind not in "iu":
+        p = pd.to_numeric(pd.Series(p), errors="raise").to_numpy()
+        if np.isnan(p.astype(np.float64)).any():
+            raise ValueError("permno contains missing values")
+    ids = p.astype(np.int64)
     if len(ids) < 2 or bool(np.all(ids[1:] >= ids[:-1])):
         return ids, None
     order = np.argsort(ids, kind="stable")

@@ -280,12 +280,13 @@ def fama_macbeth_summary(cs_results, predictor_cols, date_col="mthcaldt", nw_lag
 
 def rolling_mean(x, window=120, min_periods=60):
     """pandas rolling(window, min_periods).mean() on a row-ordered series (NaN skipped,
-    min_periods counts non-NaN), src/calc_Lewellen_2014.py:926."""
+    min_periods counts non-NaN), src/calc_Lewellen_2014.py:926.  pandas converts +-inf to
+    NaN before the window sums (Window._prep_values), so infinities are skipped too."""
     x = np.asarray(x, dtype=np.float64)
     out = np.full(x.size, np.nan)
     for i in range(x.size):
         w = x[max(0, i - window + 1):i + 1]
-        w = w[~np.isnan(w)]
+        w = w[np.isfinite(w)]
         if w.size >= min_periods:
             out[i] = w.sum() / w.size
     return out
@@ -374,15 +375,34 @@ def predictive_slope_regressions(df, forecast, return_col="retx", date_col="mthc
 # ----------------------------------------------------------------------------------------
 # Array-level pipeline (bench cpu_baseline) — the same semantics over month-sorted arrays
 # ----------------------------------------------------------------------------------------
+def standardize_segments(v, seg_off):
+    """A9 on one month-sorted column: per month z = (x - mean_t) / std_t(ddof=1) over the
+    non-NaN values (pandas groupby transform('mean') / transform('std'), as ``standardize``);
+    a month with < 2 values or zero dispersion gives NaN z."""
+    out = np.full(v.size, np.nan)
+    for t in range(len(seg_off) - 1):
+        seg = v[seg_off[t]:seg_off[t + 1]]
+        vals = seg[~np.isnan(seg)]
+        if vals.size == 0:
+            continue
+        m = vals.mean()
+        s = vals.std(ddof=1) if vals.size > 1 else np.nan
+        with np.errstate(invalid="ignore", divide="ignore"):
+            out[seg_off[t]:seg_off[t + 1]] = (seg - m) / s
+    return out
+
+
 def pipeline_arrays(cols, seg_off, me, nyse, models, fig1_model, nw_lags=4, window=120, min_periods=60,
-                    winsor=True):
+                    winsor=True, standardize=False, y_name="retx"):
     """Full C3/C4 pass on month-sorted arrays: winsorize all columns (1/99), NYSE
     universes, per (model, universe) monthly pinv OLS, FM summaries with NW, Figure-1
     rolling coefficients, lagged-rolling forecasts and predictive-slope FM summaries.
 
     cols: dict name -> float64 array (month-sorted); seg_off: int64 [T+1].
     models: dict name -> (y name, [x names], [universe levels]).  Returns a dict of
-    per-problem outputs keyed by (model, universe level)."""
+    per-problem outputs keyed by (model, universe level).
+    ``standardize`` (A9, build-defined): after winsorizing, every column except ``y_name`` is
+    replaced by its per-month z-score (standardize_segments) before the regressions."""
     T = len(seg_off) - 1
     w = {}
     for name, v in cols.items():
@@ -401,6 +421,10 @@ def pipeline_arrays(cols, seg_off, me, nyse, models, fig1_model, nw_lags=4, wind
                     seg = np.where(seg > hi, hi, seg)
                 v[seg_off[t]:seg_off[t + 1]] = seg
         w[name] = v
+    if standardize:
+        for name in w:
+            if name != y_name:
+                w[name] = standardize_segments(w[name], seg_off)
     level = np.zeros(len(me), dtype=np.int8)
     for t in range(T):
         sl = slice(seg_off[t], seg_off[t + 1])

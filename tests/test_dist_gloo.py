@@ -1,8 +1,9 @@
 """World-size-2 gloo tests (CPU) of the month-sharded path: record all-gather with uneven
-shards, the predictive sum-combine and max-over-ranks timing.  Per-rank records are
-produced by the CPU oracle standing in for the per-rank device kernels; the sharded
-result must equal the single-process one bit for bit (sharding does not change the
-per-month arithmetic)."""
+shards, the predictive sum-combine and max-over-ranks timing.  The per-rank records are
+seeded random arrays (the exchange code is data-agnostic); the gathered / combined result
+must equal the single-process arrays bit for bit.  That the real device pipeline, split by
+shard_bounds and run per range with the global chunk policy, is bit-identical to the
+unsharded run is tested on the GPU (tests/test_gpu_parity.py::test_sharded_pipeline_bit_identical)."""
 import os
 import socket
 

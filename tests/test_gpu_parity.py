@@ -204,10 +204,17 @@ def test_build_table_2_strings_golden(CL):
     assert [[str(x) for x in r] for r in t2.values.tolist()] == meta["values"]
 
 
+def _edge_inputs(g):
+    """The edge cases with the INPUT frames stored in edge.npz (the exact inputs the
+    reference saw), not regenerated: a regeneration can differ in the last ulp."""
+    for name, _, xs in cases.edge_cases():
+        yield name, frame_from(g, name + "|in_"), xs
+
+
 def test_edge_cases_golden(R):
     g = load_npz("edge.npz")
     meta = load_json("edge.json")
-    for name, df, xs in cases.edge_cases():
+    for name, df, xs in _edge_inputs(g):
         m = meta[name]
         if m["error"]:
             exc = {"MissingDataError": R.MissingDataError, "IndexError": IndexError}[m["error"]]
@@ -228,7 +235,7 @@ def test_edge_cases_golden(R):
 
 def test_inf_in_y_matches_pinv_semantics(R):
     g = load_npz("edge.npz")
-    name, df, xs = [c for c in cases.edge_cases() if c[0] == "inf_y"][0]
+    name, df, xs = [c for c in _edge_inputs(g) if c[0] == "inf_y"][0]
     got = R.run_monthly_cs_regressions(df, "retx", xs, "mthcaldt")
     exp = frame_from(g, name + "|out_")
     for c in got.columns[2:]:
@@ -278,21 +285,23 @@ def test_mid_panel_golden(R):
 
 
 # ---------------------------------------------------------------- full pipeline vs oracle
-def _pipeline_vs_oracle(E, T, N, seed, model_cols=None, fig1=True):
+def _pipeline_vs_oracle(E, T, N, seed, model_cols=None, fig1=True, standardize=False, tweak=None):
     from fmcore import lewellen as LW, synth
     model_cols = model_cols or LW.table2_models()
     a = synth.synth_arrays(T, N, seed, nan_rate=0.03, present_rate=0.9)
+    if tweak is not None:
+        tweak(a)
     cols = list(dict.fromkeys(["retx"] + [c for xs in model_cols.values() for c in xs] +
                               (LW.FIG1_VARS if fig1 else [])))
     panel = E.panel_from_arrays([a[c] for c in cols], cols, a["month"], me=a["me"], nyse=a["nyse"])
-    out = LW.run_pipeline(panel, LW.PipelineConfig(fig1=fig1), model_cols=model_cols)
+    out = LW.run_pipeline(panel, LW.PipelineConfig(fig1=fig1, standardize=standardize), model_cols=model_cols)
     seg_off = panel.seg_off_h
     srt = {c: a[c][panel.order] for c in cols}
     models = {name: ("retx", xs, (0, 1, 2)) for name, xs in model_cols.items()}
     if fig1:
         models["Figure 1"] = ("retx", LW.FIG1_VARS, (0, 2))
     ref = O.pipeline_arrays(srt, seg_off, a["me"][panel.order], a["nyse"][panel.order].astype(bool), models,
-                            None)
+                            None, standardize=standardize)
     res = out.res
     rec = res.rec.cpu().numpy()
     st = res.status.cpu().numpy()
@@ -314,6 +323,8 @@ def _pipeline_vs_oracle(E, T, N, seed, model_cols=None, fig1=True):
         for j in range(p.K + 1):
             assert_series_close(rec[fitted, k, j], r["params"][:, j], f"{name}/{p.level} param {j}")
             assert_series_close(roll[k, :len(fitted), j], r["rolling"][:, j], f"{name} roll {j}")
+        # rows past the fitted-month count are written (NaN / status 0), never left stale
+        assert np.isnan(roll[k, len(fitted):]).all() and (pst[k, len(fitted):] == 0).all(), name
         for j, x in enumerate(out.model_cols[name]):
             assert scalar_close(mean[k, 1 + j], r["summary"][x][0], RTOL, 1e-12), (name, x)
             assert scalar_close(tstat[k, 1 + j], r["summary"][x][1], RTOL, 1e-12), (name, x)
@@ -323,6 +334,7 @@ def _pipeline_vs_oracle(E, T, N, seed, model_cols=None, fig1=True):
         assert_series_close(pred[k, pf, 1], r["pred_R2"], f"{name} pred R2")
         assert scalar_close(pmean[k, 0], r["pred_summary"][0], RTOL, 1e-12)
         assert scalar_close(ptst[k, 0], r["pred_summary"][1], RTOL, 1e-12)
+    return out
 
 
 @pytest.mark.parametrize("fused", [True, False], ids=["ts_fused", "ts_per_stage"])
@@ -331,6 +343,186 @@ def test_pipeline_vs_oracle(E, fused, monkeypatch):
     if not fused:   # the per-stage kernels that serve series too long for LDS staging
         monkeypatch.setattr(E, "ts_fused_fits", lambda *a, **k: False)
     _pipeline_vs_oracle(E, 150, 400, 99)
+
+
+def _unfitted_early_months(a):
+    """Real Lewellen data has months where a Model-3-only characteristic is missing for
+    every firm (log_return_13_36 needs 36 months of history), so those problems fit fewer
+    months than the panel has (count < T)."""
+    early = a["month"] < a["month"].min() + 17
+    a["log_return_13_36"][early] = np.nan
+    a["beta"][a["month"] == a["month"].min() + 40] = np.nan
+
+
+@pytest.mark.parametrize("fused", [True, False], ids=["ts_fused", "ts_per_stage"])
+def test_pipeline_unfitted_months(E, fused, monkeypatch):
+    """problems with count < T.  The fused and per-stage time-series
+    paths must both match the oracle (incl. the predictive NW summary) and write NaN /
+    status 0 to every row past the fitted count."""
+    if not fused:
+        monkeypatch.setattr(E, "ts_fused_fits", lambda *a, **k: False)
+    out = _pipeline_vs_oracle(E, 120, 300, 41, tweak=_unfitted_early_months)
+    cnt = out.ix.count.cpu().numpy()
+    assert (cnt < out.res.status.shape[0]).any()
+
+
+def test_pipeline_unfitted_months_fused_equals_per_stage(E, monkeypatch):
+    from fmcore import lewellen as LW, synth
+    a = synth.synth_arrays(100, 250, 43, nan_rate=0.03, present_rate=0.9)
+    _unfitted_early_months(a)
+    cols = list(dict.fromkeys(["retx"] + [c for xs in LW.table2_models().values() for c in xs] + LW.FIG1_VARS))
+    panel = E.panel_from_arrays([a[c] for c in cols], cols, a["month"], me=a["me"], nyse=a["nyse"])
+    f = LW.run_pipeline(panel)
+    monkeypatch.setattr(E, "ts_fused_fits", lambda *a, **k: False)
+    s = LW.run_pipeline(panel)
+    # statuses and NaN patterns exact; values to the FP tolerance (the fused kernel slides its
+    # window sums, the per-stage one sums every window directly)
+    assert np.array_equal(f.pred_status.cpu().numpy(), s.pred_status.cpu().numpy())
+    for x, y in ((f.rolling, s.rolling), (f.pred[..., :3], s.pred[..., :3]), (f.summary.mean, s.summary.mean),
+                 (f.pred_summary.mean, s.pred_summary.mean), (f.pred_summary.tstat, s.pred_summary.tstat)):
+        x, y = x.cpu().numpy(), y.cpu().numpy()
+        for k in range(x.shape[0]):
+            assert_series_close(x[k].ravel(), y[k].ravel(), f"problem {k}")
+
+
+def _degenerate_std_months(a):
+    """A9 edge months: a predictor constant (exactly representable, so its std is exactly
+    0) in one month and present in a single row of another: z is all-NaN there."""
+    m0 = a["month"].min()
+    a["roa"][a["month"] == m0 + 3] = 0.5
+    one = np.nonzero(a["month"] == m0 + 5)[0]
+    a["log_bm"][one[1:]] = np.nan
+
+
+def test_pipeline_standardized_vs_oracle(E):
+    """A9 through the whole pass: winsorize -> per-month z-scores of every predictor (the
+    Gram's shift / inv_scale path, nothing added back) -> regressions, rolling,
+    forecasts; against the oracle's standardize-then-pinv (parity unpinned vs the
+    reference, which has no standardization)."""
+    _pipeline_vs_oracle(E, 90, 300, 17, standardize=True, tweak=_degenerate_std_months)
+
+
+def test_standardize_frame_vs_oracle(CL):
+    """A9 drop-in: calc_Lewellen_2014.standardize against the oracle's pandas transform."""
+    from fmcore import synth
+    df = synth.synth_frame(30, 200, 23, nan_rate=0.05, present_rate=0.9)
+    df = df.sample(frac=1.0, random_state=1)                # scrambled row order
+    months = np.sort(df["mthcaldt"].unique())
+    df.loc[df["mthcaldt"] == months[2], "roa"] = 0.25          # zero dispersion -> NaN z
+    df.loc[(df["mthcaldt"] == months[4]) & (df["permno"] != df["permno"].min()), "dy"] = np.nan
+    vs = ["log_size", "log_bm", "roa", "dy", "retx"]
+    got = CL.standardize(df, vs)
+    exp = O.standardize(df, vs)
+    assert list(got.index) == list(exp.index) and list(got.columns) == list(exp.columns)
+    for v in vs:
+        assert_series_close(got[v].values, exp[v].values, v)
+
+
+def test_forecast_api_vs_oracle(CL):
+    """A7/A8 per-row API: monthly_coefficients -> rolling_coefficients (host .shift(lag))
+    -> expected_return_forecasts (fm_forecast) -> predictive_slope_regressions, against
+    the oracle's monthly_params / rolling_coefficients / expected_return_forecasts /
+    predictive_slope_regressions (tolerance 1e-9 series RMS, NaN patterns exact)."""
+    from fmcore import synth
+    df = synth.synth_frame(200, 150, 29, nan_rate=0.03, present_rate=0.9)
+    xs = ["log_size", "log_bm", "return_12_2", "roa"]
+    pg = CL.monthly_coefficients(df, "retx", xs)
+    pe = O.monthly_params(df, "retx", xs)
+    assert list(pg.index) == list(pe.index) and list(pg.columns) == list(pe.columns)
+    for c in pe.columns:
+        assert_series_close(pg[c].values, pe[c].values, "params " + c)
+    for lag in (1, 3):
+        rg = CL.rolling_coefficients(pe, 120, 60, lag)
+        re_ = O.rolling_coefficients(pe, 120, 60, lag)
+        assert list(rg.index) == list(re_.index)
+        for c in re_.columns:
+            assert_series_close(rg[c].values, re_[c].values, f"rolling {c} lag {lag}")
+    roll = O.rolling_coefficients(pe, 120, 60, 1)
+    fg = CL.expected_return_forecasts(df, roll, xs)
+    fe = O.expected_return_forecasts(df, roll, xs)
+    assert list(fg.index) == list(fe.index)
+    assert_series_close(fg.values, fe.values, "forecast")
+    assert np.isfinite(fe.values).sum() > 1000
+    csg, sg = CL.predictive_slope_regressions(df, fe)
+    cse, se = O.predictive_slope_regressions(df, fe)
+    assert np.array_equal(csg["N"].values, cse["N"].values)
+    for c in ("R2", "slope_forecast"):
+        assert_series_close(csg[c].values, cse[c].values, c)
+    for k in se.index:
+        assert scalar_close(sg[k], se[k], RTOL, 1e-12), k
+
+
+def test_rolling_skips_infinite_coefficients(CL):
+    """pandas rolling().mean() turns +-inf into NaN (Window._prep_values): an inf-in-y month
+    (statsmodels' +-inf params) must not spread through the 120-row window."""
+    idx = pd.date_range("1970-01-31", periods=150, freq="ME")
+    rng = np.random.default_rng(3)
+    p = pd.DataFrame({"const": rng.normal(size=150), "x": rng.normal(size=150)}, index=idx)
+    p.iloc[70, 1] = np.inf
+    p.iloc[90, 0] = -np.inf
+    p.iloc[100, 1] = np.nan
+    got = CL.rolling_coefficients(p, 120, 60, 0)
+    exp = p.rolling(120, min_periods=60).mean()
+    for c in p.columns:
+        assert_series_close(got[c].values, exp[c].values, c)
+    assert np.isfinite(got.values[75:]).all()
+
+
+def test_sharded_pipeline_bit_identical(E):
+    """SURVEY §8(e) on one GPU: split a ragged panel into 3 month ranges with
+    dist.shard_bounds, run local_stage per range with the GLOBAL chunk policy, concatenate
+    the records, run time_series_stage per shard (global records, local moments, its
+    seg_lo/seg_hi) and SUM the predictive records -- every output must equal the unsharded
+    run_pipeline bit for bit (NaN patterns included)."""
+    import torch
+    from fmcore import dist as D, lewellen as LW, synth
+    a = synth.synth_arrays(96, 400, 13, nan_rate=0.03, present_rate=0.6)   # ragged months
+    _unfitted_early_months(a)
+    cols = list(dict.fromkeys(["retx"] + [c for xs in LW.table2_models().values() for c in xs] + LW.FIG1_VARS))
+    panel = E.panel_from_arrays([a[c] for c in cols], cols, a["month"], me=a["me"], nyse=a["nyse"])
+    cfg = LW.PipelineConfig()
+    mc = LW.table2_models()
+    full = LW.run_pipeline(panel, cfg, model_cols=mc)
+    off = panel.seg_off_h
+    ch = E.default_chunk_rows(panel.nrows, panel.nseg, panel.max_seg_len)
+    bounds = D.shard_bounds(np.diff(off), 3)
+    assert len({e - s for s, e in bounds}) > 1
+    locs = []
+    for s0, s1 in bounds:
+        r0, r1 = int(off[s0]), int(off[s1])
+        so = off[s0:s1 + 1] - off[s0]
+        sub = E.DevicePanel(cols=panel.cols[:, r0:r1].contiguous(), names=panel.names,
+                            seg_off=torch.from_numpy(so).to(panel.cols.device), seg_off_h=so,
+                            me=panel.me[r0:r1].contiguous(), nyse=panel.nyse[r0:r1].contiguous(),
+                            chunk_rows=ch)
+        locs.append(LW.local_stage(sub, cfg, mc)[0])
+    rec = torch.cat([r.rec for r in locs])
+    st = torch.cat([r.status for r in locs])
+    assert _same(rec.cpu().numpy(), full.res.rec.cpu().numpy())
+    assert np.array_equal(st.cpu().numpy(), full.res.status.cpu().numpy())
+    mom = torch.cat([r.moments for r in locs]).cpu().numpy()
+    fm_ = full.res.moments.cpu().numpy()
+    stf = full.res.status.cpu().numpy()
+    for k, p in enumerate(full.res.problems):   # fitted months: the solve writes 1 + K1 + K1^2
+        w = 1 + (p.K + 1) + (p.K + 1) ** 2
+        fit = (stf[:, k] & 1) != 0
+        assert _same(mom[fit, k, :w], fm_[fit, k, :w])
+    pred = pst = None
+    for (s0, s1), loc in zip(bounds, locs):
+        g = E.FMResult(problems=loc.problems, rec=rec, status=st, pmax=loc.pmax, moments=loc.moments,
+                       mom_stride=loc.mom_stride)
+        ix, summ, roll, p, ps = LW.time_series_stage(g, cfg, moments=loc.moments, seg_lo=s0, seg_hi=s1)
+        for x, y in ((summ.mean, full.summary.mean), (summ.tstat, full.summary.tstat), (roll, full.rolling),
+                     (ix.count, full.ix.count)):
+            assert _same(x.cpu().numpy(), y.cpu().numpy())
+        pred = p.clone() if pred is None else pred + p
+        pst = ps.clone() if pst is None else pst + ps
+    assert np.array_equal(pst.cpu().numpy(), full.pred_status.cpu().numpy())
+    keep = (full.pred_status.cpu().numpy() & 1) != 0
+    assert _same(pred.cpu().numpy()[keep], full.pred.cpu().numpy()[keep])
+    psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
+    assert _same(psumm.mean.cpu().numpy(), full.pred_summary.mean.cpu().numpy())
+    assert _same(psumm.tstat.cpu().numpy(), full.pred_summary.tstat.cpu().numpy())
 
 
 def test_pipeline_c5_month_width(E):

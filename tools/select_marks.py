@@ -1,5 +1,6 @@
 """Diagnostic: which (month, column) units does the wave select kernel hand to the fallback
-pass on the bench panel?  Run with FM_SELECT_NO_FALLBACK=1 (marks stay as nvalid == -1)."""
+pass on the bench panel?  Needs a diagnostic library built with
+-DFM_SELECT_DIAG_NO_FALLBACK (marks stay as nvalid == -1); the shipped library never is."""
 import os
 import sys
 
@@ -13,7 +14,6 @@ from fmcore import engine as E  # noqa: E402
 
 
 def main():
-    assert os.environ.get("FM_SELECT_NO_FALLBACK") == "1"
     dev = E.require_device()
     panel = E.panel_synthetic(600, 5000, 1, device=dev)
     cuts = E.select_cuts(panel, 0.01, 0.99, 5, E.LERP_NUMPY, center=True)
