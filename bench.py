@@ -188,20 +188,27 @@ def main():
     kern = {}
     for tag in timer.names():
         kern[tag] = timer.avg_ms(tag)   # events around each eager launch (incl. launch gaps)
-    dev_ms = {t: E.time_launch(t) for t in ("fm_select_cuts", "fm_gram", "fm_solve")}
-    bytes_select = rows_local * C * 8            # one read of every winsorized column
-    bytes_gram = rows_local * (C * 8 + 1)         # every column + the universe level byte
-    cand = {"fm_select_cuts": bytes_select, "fm_gram": bytes_gram}
-    dom = max(cand, key=lambda k: dev_ms[k])
+    fused = "fm_month_pass" in E.LAST_LAUNCH
+    tags = (("fm_month_pass",) if fused else ("fm_select_cuts", "fm_gram")) + \
+        ("fm_select_cuts[nyse]", "fm_solve", "fm_ts_fused")
+    dev_ms = {t: E.time_launch(t) for t in tags if t in E.LAST_LAUNCH}
+    # algorithmic HBM bytes per launch: every panel column once (8 B per
+    # value), the universe level byte, and the month tables written (cuts, pivots, Gram
+    # partials); fm_select alone reads the columns only
+    T_l = panel.nseg
+    cand = {"fm_select_cuts": rows_local * C * 8, "fm_gram": rows_local * (C * 8 + 1)}
+    if fused:
+        partial = E.LAST_LAUNCH["fm_month_pass"][2][2]          # [T, buckets, 136] Gram partials
+        cand["fm_month_pass"] = rows_local * (C * 8 + 1) + T_l * C * (3 * 8 + 4) + partial.numel() * 8
+    dom = max((t for t in cand if t in dev_ms), key=lambda k: dev_ms[k])
     dom_ms = dev_ms[dom]
     achieved = cand[dom] / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf)).get(dom)
-        except Exception:
-            traffic = None
+    traffic = _pmc_traffic(dom)
+    # whole pass: every input byte of a firm-month row -- the C FP64 columns,
+    # me (FP64) and the NYSE flag -- over the measured step time
+    b_row = C * 8 + 8 + 1
+    ms_step = dt / args.steps * 1e3
+    whole = rows_local * b_row / (ms_step * 1e-3) / 1e9
 
     result = {
         "metric": METRIC,
@@ -225,9 +232,15 @@ def main():
         },
         "regressions_per_s": nfit * args.steps / dt,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "bytes_per_launch": cand[dom], "avg_launch_ms": dom_ms},
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic["bytes"] if traffic else None,
+                     "traffic_ratio": traffic["bytes"] / cand[dom] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None,
+                     "bytes_per_launch": cand[dom], "avg_launch_ms": dom_ms,
+                     "whole_pass": {"bytes_per_row": b_row, "achieved": whole, "frac": whole / HBM_PEAK_GBS,
+                                    "ms_per_step": ms_step}},
         "kernel_ms": {k: round(v, 4) for k, v in dev_ms.items()},
+        "lib_sha16": _lib_sha(),
         "kernel_ms_eager_events": {k: round(v, 4) for k, v in kern.items()},
         "graph": not args.no_graph,
     }
@@ -241,6 +254,30 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def _lib_sha():
+    import hashlib
+    path = os.path.join(PKG, "lib", "libfm_hip.so")
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def _pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 counter summary
+    (profiles/pmc_traffic.json, tools/pmc_traffic.py: FETCH_SIZE x the gfx950 calibration +
+    WRITE_SIZE, separate --pmc passes).  Used only if it was collected on the SAME library
+    build (sha256 of libfm_hip.so): a stale file is refused, not reported."""
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(tf))
+    except Exception:
+        return None
+    if d.get("lib_sha16") != _lib_sha() or kernel not in d:
+        return None
+    return {"bytes": d[kernel], "source": f"profiles/pmc_traffic.json (lib {d['lib_sha16']})"}
 
 
 def firm_chars_stage(args, E):

@@ -463,6 +463,50 @@ def _group_plans(panel, models, problems, nlevels, cap, const_check, dev):
     return plans
 
 
+def _solve_group(panel, src, gpl, partial, seg_chunk_off, zw, nlevels, T, pmax, mom_stride, lo, hi,
+                 shift, inv_scale, add_back, level, const_check, keep):
+    """fm_solve + the statsmodels fix-ups (inf in y, nonzero constant columns) for one
+    model group; returns (rec, status, moments) [T, ng, ...]."""
+    dev = src.device
+    ng = gpl.nprob
+    rs = pmax + 2
+    grec = torch.empty((T, ng, rs), dtype=torch.float64, device=dev)
+    gst = torch.empty((T, ng), dtype=torch.int32, device=dev)   # the solve writes every entry
+    # centered moments are always produced: the inf-in-y fix reads them
+    gmom = torch.empty((T, ng, mom_stride), dtype=torch.float64, device=dev)
+    sa = L.SolveArgs(
+        partial=partial.data_ptr(), seg_chunk_off=seg_chunk_off.data_ptr(), nseg=T, zw=zw,
+        nlevels=nlevels, npatterns=gpl.npatterns, pattern_models=gpl.patm.data_ptr(), nprob=ng,
+        prob_model=gpl.pm.data_ptr(), prob_level=gpl.pl.data_ptr(), prob_z=gpl.pz.data_ptr(),
+        prob_nz=gpl.pnz.data_ptr(), prob_flags=gpl.pf.data_ptr(), add_back=_ptr(add_back),
+        gram_flags=None, nmodels=gpl.nmodels, pmax=pmax, rec=grec.data_ptr(),
+        status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride)
+    _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
+    _remember("fm_solve", "fm_solve", sa, partial, seg_chunk_off, gpl, add_back, grec, gst, gmom, *keep)
+    # inf in y: statsmodels' pinv(X) @ y gives +-inf / NaN coefficients.  The fix-up scans
+    # the status on the device (npairs = -1), so there is no host round trip.
+    _kcall("fm_inf_y_fix", "fm_inf_y_fix", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
+           _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), ng,
+           gpl.pl.data_ptr(), gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1,
+           gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), _stream())
+    # exact nonzero-constant test where the Gram flagged a near-zero variance
+    if const_check:
+        _kcall("fm_const_check", "fm_const_check", src.data_ptr(), src.stride(0), src.shape[0],
+               panel.seg_off.data_ptr(), T, _ptr(lo), _ptr(hi), _ptr(level), ng, gpl.pl.data_ptr(),
+               gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1, gst.data_ptr(), _stream())
+    return grec, gst, gmom
+
+
+def _problems(models, nlevels):
+    problems = []
+    for mi, m in enumerate(models):
+        for u in m.levels:
+            if u >= nlevels:
+                raise ValueError("model level beyond the universe levels provided")
+            problems.append(Problem(mi, u, len(m.xs)))
+    return problems
+
+
 def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, cuts: Cuts = None,
             shift=None, inv_scale=None, add_back=None, moments=False, cols=None, const_check=True):
     """One batched cross-sectional pass: every (model, universe level) problem for every
@@ -479,12 +523,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
         shift = pilot_shift(panel, src)
     if add_back is None and inv_scale is None:
         add_back = shift
-    problems = []
-    for mi, m in enumerate(models):
-        for u in m.levels:
-            if u >= nlevels:
-                raise ValueError("model level beyond the universe levels provided")
-            problems.append(Problem(mi, u, len(m.xs)))
+    problems = _problems(models, nlevels)
     pmax = max(2, max(p.K + 1 for p in problems))
     nprob = len(problems)
     rs = pmax + 2
@@ -510,31 +549,9 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
             npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr())
         _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
         _remember("fm_gram", "fm_gram", ga, src, partial, flags, lo, hi, shift, inv_scale, level, plan, gpl)
-        ng = gpl.nprob
-        grec = torch.empty((T, ng, rs), dtype=torch.float64, device=dev)
-        gst = torch.empty((T, ng), dtype=torch.int32, device=dev)   # the solve writes every entry
-        # centered moments are always produced: the inf-in-y fix reads them
-        gmom = torch.empty((T, ng, mom_stride), dtype=torch.float64, device=dev)
-        sa = L.SolveArgs(
-            partial=partial.data_ptr(), seg_chunk_off=plan.seg_chunk_off.data_ptr(), nseg=T, zw=zw,
-            nlevels=nlevels, npatterns=gpl.npatterns, pattern_models=gpl.patm.data_ptr(), nprob=ng,
-            prob_model=gpl.pm.data_ptr(), prob_level=gpl.pl.data_ptr(), prob_z=gpl.pz.data_ptr(),
-            prob_nz=gpl.pnz.data_ptr(), prob_flags=gpl.pf.data_ptr(), add_back=_ptr(add_back),
-            gram_flags=None, nmodels=gpl.nmodels, pmax=pmax, rec=grec.data_ptr(),
-            status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride)
-        _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
-        _remember("fm_solve", "fm_solve", sa, partial, plan, gpl, add_back, flags, grec, gst, gmom)
-        # inf in y: statsmodels' pinv(X) @ y gives +-inf / NaN coefficients.  The fix-up scans
-        # the status on the device (npairs = -1), so there is no host round trip.
-        _kcall("fm_inf_y_fix", "fm_inf_y_fix", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
-               _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), ng,
-               gpl.pl.data_ptr(), gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1,
-               gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), _stream())
-        # exact nonzero-constant test where the Gram flagged a near-zero variance
-        if const_check:
-            _kcall("fm_const_check", "fm_const_check", src.data_ptr(), src.stride(0), ncols,
-                   panel.seg_off.data_ptr(), T, _ptr(lo), _ptr(hi), _ptr(level), ng, gpl.pl.data_ptr(),
-                   gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1, gst.data_ptr(), _stream())
+        grec, gst, gmom = _solve_group(panel, src, gpl, partial, plan.seg_chunk_off, zw, nlevels, T, pmax,
+                                       mom_stride, lo, hi, shift, inv_scale, add_back, level,
+                                       const_check, (src, flags, lo, hi, shift, inv_scale, level, plan))
         if len(groups) == 1:
             rec, status = grec, gst
             mom = gmom if moments else None
@@ -545,6 +562,54 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
                 mom.index_copy_(1, gpl.idx, gmom)
     return FMResult(problems=problems, rec=rec, status=status, pmax=pmax, moments=mom,
                     mom_stride=mom_stride)
+
+
+def month_pass_fits(panel: DevicePanel, models: Sequence[Model], nlevels=1):
+    """Whether fm_month_pass can take this pass (<= 15 columns, one model group of <= 16
+    buckets, months of <= FM_MONTH_MAX_ROWS rows); else select_cuts + fm_pass."""
+    if panel.ncols > 15 or panel.max_seg_len > L.FM_MONTH_MAX_ROWS:
+        return False
+    if len(models) > L.FM_MAX_MODELS:
+        return False
+    return len(plan_patterns(models)[1]) * nlevels <= 16
+
+
+def month_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, q_lo=0.01, q_hi=0.99,
+               min_count=5, moments=False, const_check=True):
+    """Winsorize cuts (numpy 'linear', pivot = midpoint of the cuts) and the batched Gram of
+    every (model, universe level) problem, one workgroup per month in ONE launch
+    (fm_month_pass: the month's rows are fetched from HBM once), then the solve and the
+    statsmodels fix-ups.  Returns (FMResult, Cuts)."""
+    src = panel.cols
+    dev = src.device
+    T, C = panel.nseg, panel.ncols
+    problems = _problems(models, nlevels)
+    pmax = max(2, max(p.K + 1 for p in problems))
+    mom_stride = 1 + (pmax + 1) + (pmax + 1) ** 2
+    (gpl,) = _group_plans(panel, models, problems, nlevels, 16, const_check, dev)
+    lo = torch.empty((C, T), dtype=torch.float64, device=dev)
+    hi = torch.empty_like(lo)
+    cen = torch.empty_like(lo)
+    nv = torch.empty((C, T), dtype=torch.int32, device=dev)
+    nb = gpl.npatterns * nlevels
+    partial = torch.empty((T, nb, 136), dtype=torch.float64, device=dev)
+    ga = L.GramArgs(
+        cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, nseg=T, seg_off=panel.seg_off.data_ptr(),
+        chunk_seg=None, chunk_row=None, nchunks=T, lo=None, hi=None, shift=None, inv_scale=None,
+        level=_ptr(level), nlevels=nlevels, model_mask=gpl.mm.data_ptr(), model_ymask=gpl.ym.data_ptr(),
+        nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(), npatterns=gpl.npatterns,
+        partial=partial.data_ptr(), flags=None)
+    ma = L.MonthArgs(gram=ga, q_lo=float(q_lo), q_hi=float(q_hi), min_count=int(min_count),
+                     max_seg_len=max(panel.max_seg_len, 1), lo=lo.data_ptr(), hi=hi.data_ptr(),
+                     nvalid=nv.data_ptr(), center=cen.data_ptr())
+    _kcall("fm_month_pass", "fm_month_pass", L.C.byref(ma), _stream())
+    _remember("fm_month_pass", "fm_month_pass", ma, src, level, partial, lo, hi, cen, nv, gpl, panel.seg_off)
+    soff = _small_tensor(tuple(range(T + 1)), torch.int32, dev)
+    rec, st, mom = _solve_group(panel, src, gpl, partial, soff, 16, nlevels, T, pmax, mom_stride, lo, hi,
+                                cen, None, cen, level, const_check, (src, lo, hi, cen, level))
+    res = FMResult(problems=problems, rec=rec, status=st, pmax=pmax, moments=mom if moments else None,
+                   mom_stride=mom_stride)
+    return res, Cuts(lo, hi, nv, center=cen)
 
 
 def drop_degenerate_months(res: FMResult, models: Sequence[Model], sd):

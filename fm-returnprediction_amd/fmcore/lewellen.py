@@ -72,6 +72,9 @@ class PipelineConfig:
     lag: int = 1
     forecasts: bool = True
     fig1: bool = True
+    # one launch per pass for the winsorize cuts + batched Gram (fm_month_pass) instead of
+    # fm_select + fm_gram; off by default until it is the faster of the two
+    fused_month: bool = False
 
 
 @dataclass
@@ -141,6 +144,19 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
     nlevels = 1
     main = torch.cuda.current_stream()
     side = None
+    models, names = build_models(panel, model_cols, y=y, fig1=cfg.fig1, universes=cfg.universes)
+    if cfg.fused_month and cfg.winsorize and not cfg.standardize and \
+            E.month_pass_fits(panel, models, 3 if cfg.universes else 1):
+        # fused path: NYSE breakpoints + universe levels, then ONE launch per pass doing the
+        # winsorize cuts and the batched Gram month by month (fm_month_pass)
+        if cfg.universes:
+            a, b = E.nyse_breakpoints(panel)
+            level = E.universe_level(panel, a, b)
+            nlevels = 3
+            bp = (a, b)
+        res, cuts = E.month_pass(panel, models, level=level, nlevels=nlevels, q_lo=cfg.lower_percentile / 100,
+                                 q_hi=cfg.upper_percentile / 100, min_count=5, moments=cfg.forecasts)
+        return res, names, cuts, level, bp
     if cfg.universes:
         side = _side_stream(main.device)
         side.wait_stream(main)
@@ -166,7 +182,6 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
                           cuts.nvalid, cuts.mean, cuts.sd, cuts.center)
     if side is not None:
         main.wait_stream(side)
-    models, names = build_models(panel, model_cols, y=y, fig1=cfg.fig1, universes=cfg.universes)
     res = E.fm_pass(panel, models, level=level, nlevels=nlevels, cuts=cuts, shift=shift,
                     inv_scale=inv_scale, add_back=add_back if cfg.standardize else shift,
                     moments=cfg.forecasts)

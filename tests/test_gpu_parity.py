@@ -107,6 +107,74 @@ def test_percentile_tails_adversarial(E, wave_path):
             assert _same([lo[t]], [ra]) and _same([hi[t]], [rb]), (qa, qb, t, len(v), lo[t], ra, hi[t], rb)
 
 
+def _hard_segment(rng, n, kind):
+    if kind == "t2":
+        x = rng.standard_t(2, n)
+        x[rng.random(n) < 0.2] = np.nan
+        x[:3] = [np.inf, -np.inf, -0.0]
+        return x
+    if kind == "ties":
+        return rng.integers(-2, 3, n).astype(np.float64) * 0.5
+    if kind == "const":
+        return np.full(n, 2.5)
+    if kind == "cluster":     # > HCAP keys inside one level-1 bin: the refinement levels
+        x = 1.0 + rng.integers(0, 4000, n) * np.finfo(np.float64).eps
+        x[rng.random(n) < 0.01] = -1e300
+        x[rng.random(n) < 0.01] = 1e300
+        return x
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("n", [30000, 100000, 1000000])
+def test_long_segment_cuts_bit_exact(E, n):
+    """Segments longer than the 24,576-row register budget stream from HBM (adaptive
+    histogram select): bit-exact against np.percentile and the pandas group-quantile lerp,
+    on heavy tails with NaN / +-inf / -0.0, heavy ties, a constant segment and clustered
+    keys behind extreme outliers, next to a short segment."""
+    rng = np.random.default_rng(n)
+    kinds = ["t2", "ties", "const", "cluster"]
+    segs = [_hard_segment(rng, n, k) for k in kinds] + [rng.standard_normal(777)]
+    vals = np.concatenate(segs)
+    labels = np.repeat(np.arange(len(segs)), [len(x) for x in segs])
+    panel = E.panel_from_arrays([vals], ["v"], labels)
+    for qa, qb in ((1, 99), (0, 100), (20, 50)):
+        cuts = E.select_cuts(panel, qa / 100, qb / 100, 1, E.LERP_NUMPY)
+        lo, hi = cuts.lo.cpu().numpy()[0], cuts.hi.cpu().numpy()[0]
+        for t, x in enumerate(segs):
+            v = x[~np.isnan(x)]
+            with np.errstate(invalid="ignore"):
+                ra, rb = np.percentile(v, qa), np.percentile(v, qb)
+            assert _same([lo[t]], [ra]) and _same([hi[t]], [rb]), (kinds + ["short"])[t]
+    cuts = E.select_cuts(panel, 0.2, 0.5, 1, E.LERP_PANDAS)
+    lo, hi = cuts.lo.cpu().numpy()[0], cuts.hi.cpu().numpy()[0]
+    for t, x in enumerate(segs):
+        y = np.where(np.isfinite(x), x, np.nan) if t == 0 else x
+        if t == 0:
+            continue    # pandas' quantile of +-inf rows is not the lerp's business
+        assert _same([lo[t]], [O.pandas_quantile(y, 0.2)]) and _same([hi[t]], [O.pandas_quantile(y, 0.5)])
+
+
+def test_masked_middle_quantiles_hist_select(E):
+    """NYSE-style row-masked middle quantiles (pandas lerp) through the workgroup path's
+    adaptive histogram select, incl. clustered keys that need the refinement levels."""
+    rng = np.random.default_rng(5)
+    segs, masks = [], []
+    for n in (1, 2, 7, 300, 5000, 20000):
+        for kind in ("lognormal", "cluster", "ties"):
+            x = np.exp(rng.normal(5, 2, n)) if kind == "lognormal" else _hard_segment(rng, n, kind)
+            segs.append(x)
+            masks.append(rng.random(n) < 0.4)
+    vals = np.concatenate(segs)
+    mask = np.concatenate(masks).astype(np.uint8)
+    labels = np.repeat(np.arange(len(segs)), [len(x) for x in segs])
+    panel = E.panel_from_arrays([vals], ["me"], labels, me=vals, nyse=mask)
+    a, b = E.nyse_breakpoints(panel)
+    a, b = a.cpu().numpy(), b.cpu().numpy()
+    for t, (x, m) in enumerate(zip(segs, masks)):
+        assert _same([a[t]], [O.pandas_quantile(x[m], 0.2)]), t
+        assert _same([b[t]], [O.pandas_quantile(x[m], 0.5)]), t
+
+
 def test_pandas_quantile_bit_exact(E):
     g = load_npz("pct.npz")
     vals, off, ref = g["values"], g["offsets"], g["pd_quantile"]

@@ -1,0 +1,49 @@
+"""Kernel A/B timing on the bench panel: python tools/kbench.py [lib.so ...]
+Each library (default: the in-tree one) runs in its own subprocess (FM_HIP_LIB); one
+pipeline pass fills engine.LAST_LAUNCH, then every tag's latest launch is re-issued back to
+back (engine.time_launch) several times; the median per tag is printed."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child():
+    sys.path[:0] = [os.path.join(ROOT, "fm-returnprediction_amd"), ROOT]
+    import numpy as np
+    import torch
+    from fmcore import engine as E
+    from fmcore import lewellen as LW
+    dev = E.require_device()
+    panel = E.panel_synthetic(600, 5000, 1, device=dev)
+    fused = os.environ.get("KB_FUSED") == "1"
+    cfg = LW.PipelineConfig(fused_month=fused)
+    for _ in range(3):
+        LW.run_pipeline(panel, cfg)
+    torch.cuda.synchronize()
+    out = {}
+    for tag in sorted(E.LAST_LAUNCH):
+        ts = [E.time_launch(tag, 10) for _ in range(7)]
+        out[tag] = float(np.median(ts))
+    print("KB " + json.dumps(out))
+
+
+def main():
+    if os.environ.get("KB_CHILD") == "1":
+        return child()
+    libs = sys.argv[1:] or [os.path.join(ROOT, "fm-returnprediction_amd", "lib", "libfm_hip.so")]
+    for lib in libs:
+        env = dict(os.environ, KB_CHILD="1", FM_HIP_LIB=os.path.abspath(lib))
+        r = subprocess.run([sys.executable, __file__], env=env, capture_output=True, text=True, timeout=300)
+        line = [l for l in r.stdout.splitlines() if l.startswith("KB ")]
+        if not line:
+            print(lib, "FAILED", r.stderr[-2000:])
+            continue
+        d = json.loads(line[0][3:])
+        print(os.path.basename(lib), " ".join(f"{k}={v * 1e3:.1f}us" for k, v in d.items()), flush=True)
+
+
+if __name__ == "__main__":
+    main()
