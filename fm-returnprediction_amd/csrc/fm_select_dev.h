@@ -336,19 +336,52 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
         done[t] = t >= nr;
         out[t] = kmin;
     }
-    for (int level = 0; level < 8; ++level) {
+    bool shrink[4] = {false, false, false, false};
+    // at most 4 groups x 6 levels (11 bits each) are ever needed; the bound only guards
+    for (int it = 0; it < 32; ++it) {
         int t0 = -1;
 #pragma unroll
         for (int t = 3; t >= 0; --t)
             if (!done[t]) t0 = t;
         if (t0 < 0) break;   // block-uniform
         uint64_t lo = tlo[0], hi = thi[0];
+        bool shr = false;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-            if (t == t0) lo = tlo[t], hi = thi[t];
+            if (t == t0) lo = tlo[t], hi = thi[t], shr = shrink[t];
         bool grp[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) grp[t] = !done[t] && tlo[t] == lo && thi[t] == hi;
+        if (shr) {
+            // a refined bin: shrink its range to the keys actually present (a bin of equal
+            // keys -- ties -- is answered right here)
+            uint64_t mn = SENT, mx = 0;
+            for_each([&](double x) {
+                if (!isnan(x)) {
+                    const uint64_t k = dkey(x);
+                    if (k >= lo && k <= hi) {
+                        mn = k < mn ? k : mn;
+                        mx = k > mx ? k : mx;
+                    }
+                }
+            });
+            mn = block_min_u64<SNW>(mn, sm.u64s);
+            mx = block_max_u64<SNW>(mx, sm.u64s + SNW);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (grp[t]) {
+                    tlo[t] = mn;
+                    thi[t] = mx;
+                    shrink[t] = false;
+                    if (mn == mx) {
+                        out[t] = mn;
+                        done[t] = true;
+                    }
+                }
+            lo = mn;
+            hi = mx;
+            if (mn == mx) continue;   // block-uniform
+        }
         const uint64_t span = hi - lo;
         const int shift = span < (uint64_t)HB ? 0 : 64 - __clzll(span) - 11;   // span >> shift < HB
         for (int i = tid; i < HB; i += ST) sm.hist[i] = 0u;
@@ -408,6 +441,7 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
                 tlo[t] = blo[t];
                 thi[t] = bhi[t];
                 tr[t] -= below;
+                shrink[t] = true;
             }
         }
         if (!any_list) continue;
