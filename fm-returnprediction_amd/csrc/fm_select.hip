@@ -258,6 +258,339 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Two waves per (segment, column) unit (a 128-thread workgroup per unit at a time): each wave
+// holds HALF the segment (rows (2v + h) * 64 + lane), so a wave needs half the registers of
+// select_wave_kernel, four waves per SIMD fit, and each wave sorts ONE tail:
+//   1. per wave: count, lane minima / maxima, the 64 lane-minimum high words sorted (and the
+//      complemented lane-maximum high words), all published in LDS;
+//   2. wave 0: T_lo = the j0-th smallest of the 128 lane-minimum high words (merge ranks of
+//      two sorted lists by binary search) and tau_lo = the largest lane minimum (of either
+//      wave) with that high word; wave 1 the same for the upper tail;
+//   3. per wave: values < tau_lo / > tau_hi compacted into its own LDS lists; the next
+//      unit's loads are issued here;
+//   4. wave 0 sorts the two low-tail lists together and reads ranks i0, j0; wave 1 the high
+//      tail.
+// A unit the tail path cannot decide (ranks >= 128, candidate overflow) is finished in the
+// same workgroup by the adaptive histogram select on the register values (hist_select_t),
+// so no fallback launch follows.  With universes (PairArgs::me), the first nseg units are
+// the months' NYSE `me` breakpoints (pandas lerp, nyse row mask: hist_select_t) and the
+// workgroup then writes the month's universe level bytes from the same registers, which
+// replaces the separate breakpoint / level launches of get_subsets.
+struct PairArgs {
+    SelArgs a;
+    const double* me;      // [rows] or NULL (no universe units)
+    const uint8_t* nyse;   // [rows]
+    double qa, qb;         // pandas quantiles (0.2, 0.5)
+    double* cut_a;         // [nseg]
+    double* cut_b;
+    uint8_t* level;        // [rows]
+};
+
+constexpr int PHB = 1024;   // pair kernel hist_select: bins
+constexpr int PCAP = 128;   // pair kernel hist_select: keys per list
+
+struct PairSmem {
+    union {
+        struct {
+            uint32_t sk[2][2][WAVE];   // [wave][lo / hi][lane] sorted high words
+            double ext[2][2][WAVE];    // [wave][min / max][lane] lane extrema
+            double cand[2][2][WCAP];   // [wave][lo / hi] tail candidates
+        };
+        struct {
+            uint32_t hist[PHB];
+            uint64_t buf[4 * PCAP];
+        };
+    };
+    int ni[2][4];
+    double tv[2];
+    double res[2];
+    int okv[2];
+    int hs[12];
+    uint32_t hcnt[4];
+    int ints[8];
+    uint64_t u64s[4];
+};
+
+template <int VPH>
+__global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(PairArgs pa) {
+    const SelArgs& a = pa.a;
+    __shared__ PairSmem sm;
+    const int lane = lane_id();
+    const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+    const int nuni = pa.me ? a.nseg : 0;             // universe units first (the slow ones)
+    const int64_t nunits = (int64_t)a.nseg * a.ncols + nuni;
+    int64_t k = blockIdx.x;
+    if (k >= nunits) return;   // block-uniform
+    double xv[VPH];
+    uint64_t mbits = ~0ull;    // universe units: NYSE row bits of this thread's values
+    int s_cur = 0;
+    auto load = [&](int64_t kk) -> int {
+        int s, c;
+        const double* base;
+        if (kk < nuni) {
+            s = (int)kk;
+            c = 0;
+            base = pa.me;
+        } else {
+            const int64_t u = unit_of(a, kk - nuni);
+            s = (int)(u % a.nseg);
+            c = (int)(u / a.nseg);
+            base = a.cols + (int64_t)c * a.col_stride;
+        }
+        const int64_t r0 = a.seg_off[s];
+        const int L = (int)(a.seg_off[s + 1] - r0);
+        typedef const __attribute__((address_space(1))) char* gptr;
+        const gptr b = (gptr)(base + r0);
+        const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
+        uint32_t lb = (uint32_t)(h * WAVE + lane) * 8u;
+        asm volatile("" : "+v"(lb));
+#pragma unroll
+        for (int v = 0; v < VPH; ++v) {
+            const uint32_t off = lb + (uint32_t)(v * 2 * WAVE * 8);
+            xv[v] = *(const __attribute__((address_space(1))) double*)(b + (off < lastb ? off : lastb));
+        }
+        return L;
+    };
+    int L = load(k);
+    while (true) {
+        const bool uni = k < nuni;   // block-uniform
+        int s = 0, c = 0;
+        int64_t u = 0;
+        if (uni) {
+            s = (int)k;
+        } else {
+            u = unit_of(a, k - nuni);
+            s = (int)(u % a.nseg);
+            c = (int)(u / a.nseg);
+        }
+        (void)c;
+        const int64_t kn = k + gridDim.x;
+        const bool more = kn < nunits;
+        int Ln = 0;
+        int row0 = h * WAVE + lane;
+        asm volatile("" : "+v"(row0));
+        mbits = ~0ull;
+        if (uni) {
+            // NYSE rows of this thread's values (row (2v + h) * 64 + lane of the month)
+            const uint8_t* nb = pa.nyse + a.seg_off[s];
+            mbits = 0;
+            if (L > 0) {
+#pragma unroll
+                for (int v = 0; v < VPH; ++v) {
+                    const int r = row0 + v * 2 * WAVE;
+                    const bool in = nb[r < L ? r : L - 1] != 0 && r < L;
+                    mbits |= (uint64_t)in << v;
+                }
+            }
+        }
+        // ---- 1. this wave's half: count, lane extrema (NaN = absent / masked out)
+        int nh = 0;
+        double mn4[4] = {NAN, NAN, NAN, NAN}, mx4[4] = {NAN, NAN, NAN, NAN};
+#pragma unroll
+        for (int v = 0; v < VPH; ++v) {
+            if (row0 + v * 2 * WAVE >= L) xv[v] = NAN;   // past the segment end
+            const double x = (mbits >> v) & 1 ? xv[v] : NAN;
+            nh += (int)__popcll(__ballot(!isnan(x)));
+            mn4[v & 3] = hw_min(mn4[v & 3], x);
+            mx4[v & 3] = hw_max(mx4[v & 3], x);
+        }
+        const double mn = hw_min(hw_min(mn4[0], mn4[1]), hw_min(mn4[2], mn4[3]));
+        const double mx = hw_max(hw_max(mx4[0], mx4[1]), hw_max(mx4[2], mx4[3]));
+        nh = __builtin_amdgcn_readfirstlane(nh);
+        const double q_lo = uni ? pa.qa : a.q_lo, q_hi = uni ? pa.qb : a.q_hi;
+        const int mode = uni ? 1 : a.lerp_mode;
+        const int minc = uni ? 1 : a.min_count;
+        bool fast = !uni;
+        if (fast) {
+            const uint32_t ha = isnan(mn) ? 0xFFFFFFFFu : (uint32_t)(dkey(mn) >> 32);
+            const uint32_t hb = isnan(mx) ? 0xFFFFFFFFu : (uint32_t)(~dkey(mx) >> 32);
+            uint32_t ta[1] = {ha}, tb[1] = {hb};
+            wave_sort32<1>(ta);
+            wave_sort32<1>(tb);
+            sm.sk[h][0][lane] = ta[0];
+            sm.sk[h][1][lane] = tb[0];
+            sm.ext[h][0][lane] = mn;
+            sm.ext[h][1][lane] = mx;
+        }
+        if (lane == 0) sm.ni[h][0] = nh;
+        __syncthreads();
+        const int n = sm.ni[0][0] + sm.ni[1][0];
+        const bool apply = n >= minc && n > 0;
+        int i0 = 0, j0 = 0, i1 = 0, j1 = 0;
+        double g0 = 0.0, g1 = 0.0;
+        if (apply) {
+            qranks(n, q_lo, mode, i0, j0, g0);
+            qranks(n, q_hi, mode, i1, j1, g1);
+        }
+        bool ok = fast && apply;
+        if (ok) {
+            // ---- 2. this wave's tail: h == 0 low (rank j0 over lane minima), h == 1 high
+            const int kr = h == 0 ? j0 : n - 1 - i1;
+            ok = kr < 2 * WAVE;
+            if (ok) {
+                const int t = h;   // list kind
+                const uint32_t mine = sm.sk[0][t][lane], other = sm.sk[1][t][lane];
+                // merged ranks: entries of list 0 precede equal entries of list 1
+                const int r0 = lane + count_below_u32(sm.sk[1][t], mine, false);
+                const int r1 = lane + count_below_u32(sm.sk[0][t], other, true);
+                uint32_t T = 0xFFFFFFFFu;
+                const uint64_t m0 = __ballot(r0 == kr), m1 = __ballot(r1 == kr);
+                if (m0) T = (uint32_t)__builtin_amdgcn_readlane((int)mine, __builtin_ctzll(m0));
+                else if (m1) T = (uint32_t)__builtin_amdgcn_readlane((int)other, __builtin_ctzll(m1));
+                ok = T != 0xFFFFFFFFu;
+                // tau: the extreme lane extremum (either wave) whose high word is T
+                double best = NAN;
+#pragma unroll
+                for (int w2 = 0; w2 < 2; ++w2) {
+                    const double e = sm.ext[w2][t][lane];
+                    const uint32_t hw = isnan(e) ? 0xFFFFFFFFu
+                                                 : (t == 0 ? (uint32_t)(dkey(e) >> 32) : (uint32_t)(~dkey(e) >> 32));
+                    const double cv = hw == T ? e : NAN;
+                    best = t == 0 ? hw_max(best, cv) : hw_min(best, cv);
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1)
+                    best = t == 0 ? hw_max(best, xor_lanes_f64(best, o)) : hw_min(best, xor_lanes_f64(best, o));
+                if (lane == 0) sm.tv[h] = best;
+            }
+            if (lane == 0) sm.okv[h] = ok ? 1 : 0;
+            __syncthreads();
+            ok = sm.okv[0] != 0 && sm.okv[1] != 0;   // block-uniform
+        }
+        double lo = NAN, hi = NAN;
+        if (ok) {
+            // ---- 3. compaction of this wave's half into its own lists
+            int clo = 0, chi = 0;
+            const double tlo = sm.tv[0], thi = sm.tv[1];
+            double* Ll = sm.cand[h][0];
+            double* Lh = sm.cand[h][1];
+#pragma unroll
+            for (int v = 0; v < VPH; ++v) {
+                const bool bl = xv[v] < tlo, bh = xv[v] > thi;
+                const uint64_t ml = __ballot(bl), mh = __ballot(bh);
+                if (ml) {
+                    if (bl) Ll[(clo + mask_rank(ml)) & (WCAP - 1)] = xv[v];
+                    clo += (int)__popcll(ml);
+                }
+                if (mh) {
+                    if (bh) Lh[(chi + mask_rank(mh)) & (WCAP - 1)] = -xv[v];   // ascending
+                    chi += (int)__popcll(mh);
+                }
+            }
+            if (lane == 0) {
+                sm.ni[h][1] = clo;
+                sm.ni[h][2] = chi;
+            }
+            __syncthreads();
+            // ---- 4. one tail per wave over both halves' candidates
+            const int t = h;
+            const int c0 = sm.ni[0][1 + t], c1 = sm.ni[1][1 + t];
+            const int cc = c0 + c1;
+            const bool fits = c0 <= WCAP && c1 <= WCAP && cc <= 4 * WAVE;
+            if (fits) {
+                double va = NAN, vb = NAN;
+                const int ra = t == 0 ? i0 : n - 1 - j1, rb = t == 0 ? j0 : n - 1 - i1;
+                const double tau = t == 0 ? sm.tv[0] : -sm.tv[1];
+                if (cc <= 2 * WAVE) pick_tail2<2>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, tau, va, vb);
+                else pick_tail2<4>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, tau, va, vb);
+                if (lane == 0) sm.res[h] = t == 0 ? qlerp(va, vb, g0, mode) : qlerp(-vb, -va, g1, mode);
+            }
+            if (lane == 0) sm.okv[h] = fits ? 1 : 0;
+            __syncthreads();
+            ok = sm.okv[0] != 0 && sm.okv[1] != 0;   // block-uniform
+            lo = sm.res[0];
+            hi = sm.res[1];
+        }
+        if (apply && !ok) {
+            // ---- exact adaptive histogram select on the register values: universe units
+            // (middle ranks) and the rare tails the path above cannot decide
+            uint64_t kmn = SENT, kmx = 0;
+#pragma unroll
+            for (int v = 0; v < VPH; ++v) {
+                const double x = (mbits >> v) & 1 ? xv[v] : NAN;
+                if (!isnan(x)) {
+                    const uint64_t kk = dkey(x);
+                    kmn = kk < kmn ? kk : kmn;
+                    kmx = kk > kmx ? kk : kmx;
+                }
+            }
+            __syncthreads();   // the fast path's LDS (aliased by the histogram) is dead
+            kmn = block_min_u64<2>(kmn, sm.u64s);
+            kmx = block_max_u64<2>(kmx, sm.u64s + 2);
+            const int rk[4] = {i0, j0, i1, j1};
+            uint64_t ko[4];
+            hist_select_t<2, PHB, PCAP>([&](auto&& f) {
+#pragma unroll
+                for (int v = 0; v < VPH; ++v) f((mbits >> v) & 1 ? xv[v] : NAN);
+            }, 4, rk, kmn, kmx, ko, sm);
+            lo = qlerp(kval(ko[0]), kval(ko[1]), g0, mode);
+            hi = qlerp(kval(ko[2]), kval(ko[3]), g1, mode);
+        }
+        if (uni) {
+            // me_20 / me_50 and the month's universe levels (NaN me or cut: comparison false)
+            if (threadIdx.x == 0) {
+                pa.cut_a[s] = lo;
+                pa.cut_b[s] = hi;
+            }
+            uint8_t* lv = pa.level + a.seg_off[s];
+#pragma unroll
+            for (int v = 0; v < VPH; ++v) {
+                const int r = row0 + v * 2 * WAVE;
+                if (r < L) lv[r] = (uint8_t)((xv[v] >= lo ? 1 : 0) + (xv[v] >= hi ? 1 : 0));
+            }
+        } else if (h == 0) {
+            double cen = 0.5 * (lo + hi);
+            if (!isfinite(cen)) {
+                double m1 = NAN, m2 = NAN;
+#pragma unroll
+                for (int v = 0; v < VPH; ++v) {
+                    m1 = hw_min(m1, isfinite(xv[v]) ? xv[v] : NAN);
+                    m2 = hw_max(m2, isfinite(xv[v]) ? xv[v] : NAN);
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    m1 = hw_min(m1, xor_lanes_f64(m1, o));
+                    m2 = hw_max(m2, xor_lanes_f64(m2, o));
+                }
+                if (lane == 0) sm.res[0] = m1, sm.res[1] = m2;
+            }
+            if (lane == 0) {
+                if (a.center && isfinite(cen)) a.center[u] = cen;
+                a.lo[u] = lo;
+                a.hi[u] = hi;
+                if (a.nvalid) a.nvalid[u] = n;
+            }
+        } else if (!isfinite(0.5 * (lo + hi))) {
+            // wave 1's half of the finite range for the pivot fallback
+            double m1 = NAN, m2 = NAN;
+#pragma unroll
+            for (int v = 0; v < VPH; ++v) {
+                m1 = hw_min(m1, isfinite(xv[v]) ? xv[v] : NAN);
+                m2 = hw_max(m2, isfinite(xv[v]) ? xv[v] : NAN);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                m1 = hw_min(m1, xor_lanes_f64(m1, o));
+                m2 = hw_max(m2, xor_lanes_f64(m2, o));
+            }
+            if (lane == 0) sm.tv[0] = m1, sm.tv[1] = m2;
+        }
+        if (more) Ln = load(kn);   // xv is dead: the next unit's loads fly across the barrier
+        __syncthreads();
+        if (!uni && a.center && !isfinite(0.5 * (lo + hi)) && threadIdx.x == 0) {
+            // pivot fallback: the midpoint of the finite range (both halves), else 0
+            const double m1 = hw_min(sm.res[0], sm.tv[0]), m2 = hw_max(sm.res[1], sm.tv[1]);
+            double cen = 0.5 * (m1 + m2);
+            a.center[u] = isfinite(cen) ? cen : 0.0;
+        }
+        __syncthreads();   // LDS state is rewritten by the next unit
+        if (!more) break;
+        k = kn;
+        L = Ln;
+    }
+}
+
 int select_wave_grid(int64_t nunits) {
     static int ncu = [] {
         int dev = 0, n = 0;
@@ -271,6 +604,45 @@ int select_wave_grid(int64_t nunits) {
     return (int)(need < cap ? need : cap);
 }
 
+template <int VPH>
+void launch_select_pair(const PairArgs& a, hipStream_t st) {
+    static int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int64_t nunits = (int64_t)a.a.nseg * a.a.ncols + (a.me ? a.a.nseg : 0);
+    const int64_t cap = (int64_t)ncu * 8;   // eight 2-wave workgroups per CU (4 waves / SIMD)
+    hipLaunchKernelGGL((select_pair_kernel<VPH>), dim3((unsigned)(nunits < cap ? nunits : cap)), dim3(2 * WAVE),
+                       0, st, a);
+}
+
+int launch_select_pair_vph(const PairArgs& pa, int max_seg_len, hipStream_t st) {
+    const int vph = (max_seg_len + 2 * WAVE - 1) / (2 * WAVE);
+    if (vph <= 8) launch_select_pair<8>(pa, st);
+    else if (vph <= 16) launch_select_pair<16>(pa, st);
+    else if (vph <= 24) launch_select_pair<24>(pa, st);
+    else if (vph <= 32) launch_select_pair<32>(pa, st);
+    else if (vph <= 40) launch_select_pair<40>(pa, st);
+    else if (vph <= 48) launch_select_pair<48>(pa, st);
+    else {
+        set_error("select pair kernel: %d-row segments exceed %d", max_seg_len, 48 * 2 * WAVE);
+        return FM_ETOOBIG;
+    }
+    return FM_OK;
+}
+
+// A/B switch for timing builds only (-DFM_AB_SELECT_ONE_WAVE=1): the one-wave kernel
+bool getenv_flag_one_wave() {
+#ifdef FM_AB_SELECT_ONE_WAVE
+    return FM_AB_SELECT_ONE_WAVE != 0;
+#else
+    return false;
+#endif
+}
+
 template <int VPL>
 void launch_select_wave(const SelArgs& a, hipStream_t st) {
     const int64_t nunits = (int64_t)a.nseg * a.ncols;
@@ -282,6 +654,36 @@ void launch_select_wave(const SelArgs& a, hipStream_t st) {
 
 }  // namespace
 }  // namespace fm
+
+extern "C" int fm_select_universe(const fm_select_args* args, const double* me, const uint8_t* nyse,
+                                  double q_a, double q_b, double* cut_a, double* cut_b, uint8_t* level,
+                                  void* stream) {
+    using namespace fm;
+    FM_REQUIRE(args != nullptr, "fm_select_universe: null args");
+    const fm_select_args& x = *args;
+    FM_REQUIRE(x.cols && x.seg_off && x.lo && x.hi && x.nvalid && me && nyse && cut_a && cut_b && level,
+               "fm_select_universe: null pointer");
+    FM_REQUIRE(x.ncols > 0 && x.ncols <= 65535 && x.nseg >= 0, "fm_select_universe: bad sizes");
+    FM_REQUIRE(x.row_mask == nullptr && x.mean == nullptr && x.sd == nullptr,
+               "fm_select_universe: no row mask / moments (use fm_select)");
+    FM_REQUIRE(x.lerp_mode == 0 || x.lerp_mode == 1, "fm_select_universe: lerp_mode must be 0 or 1");
+    FM_REQUIRE(x.q_lo >= 0.0 && x.q_lo <= 1.0 && x.q_hi >= 0.0 && x.q_hi <= 1.0 && q_a >= 0.0 && q_a <= 1.0 &&
+                   q_b >= 0.0 && q_b <= 1.0,
+               "fm_select_universe: quantiles must be in [0,1]");
+    if (x.max_seg_len > FM_SELECT_UNIVERSE_MAX_ROWS) {
+        set_error("fm_select_universe: %d-row months exceed %d (use fm_select + fm_universe_level)",
+                  x.max_seg_len, FM_SELECT_UNIVERSE_MAX_ROWS);
+        return FM_ETOOBIG;
+    }
+    if (x.nseg == 0) return FM_OK;
+    SelArgs a{x.cols,        x.col_stride, x.seg_off, x.nseg,    x.ncols, nullptr, x.q_lo, x.q_hi,
+              x.min_count, x.lerp_mode,  x.lo,      x.hi,      x.nvalid, nullptr, nullptr, x.center};
+    PairArgs pa{a, me, nyse, q_a, q_b, cut_a, cut_b, level};
+    const int rc = launch_select_pair_vph(pa, x.max_seg_len > 0 ? x.max_seg_len : 1, (hipStream_t)stream);
+    if (rc != FM_OK) return rc;
+    FM_CHECK_LAUNCH("fm_select_universe");
+    return FM_OK;
+}
 
 extern "C" int fm_select_cuts(const double* cols, int64_t col_stride, int32_t ncols,
                               const int64_t* seg_off, int32_t nseg, int32_t max_seg_len,
@@ -322,8 +724,21 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
     // wave fast path: no row mask, segments of <= 96 * 64 rows, nvalid present (it carries
     // the fallback marks); the workgroup kernel then redoes the marked units only
     const int vpl = (max_seg_len + WAVE - 1) / WAVE;
+#ifdef FM_AB_SELECT_WG
+    const bool wave = false;   // A/B timing builds only: the workgroup-per-unit kernel for all
+#else
     const bool wave = row_mask == nullptr && nvalid != nullptr && vpl <= 96;
-    if (wave) {
+#endif
+    (void)vpl;
+    if (wave && x.mean == nullptr && vpl <= 96 && !getenv_flag_one_wave()) {
+        // two waves per unit (the common Table-2 case: no moments), self-contained: no
+        // fallback launch follows
+        PairArgs pa{a, nullptr, nullptr, 0.0, 0.0, nullptr, nullptr, nullptr};
+        const int rc = launch_select_pair_vph(pa, max_seg_len, st);
+        if (rc != FM_OK) return rc;
+        FM_CHECK_LAUNCH("fm_select_cuts(pair)");
+        return FM_OK;
+    } else if (wave) {
         if (vpl <= 16) launch_select_wave<16>(a, st);
         else if (vpl <= 32) launch_select_wave<32>(a, st);
         else if (vpl <= 48) launch_select_wave<48>(a, st);

@@ -321,9 +321,10 @@ __device__ __forceinline__ void wave_sort_lds(uint64_t* buf, int c) {
 // `for_each(f)` calls f(x) for each of this thread's values (NaN = absent): register-resident
 // values or a grid-stride stream over HBM (long segments), the same code either way.  n,
 // kmin, kmax describe the non-NaN values; block-uniform control flow; barriers inside.
-template <typename ForEach>
-__device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const int* rk, uint64_t kmin,
-                                            uint64_t kmax, uint64_t* out, SelSmem& sm) {
+template <int NW, int HBN, int CAP, typename Sm, typename ForEach>
+__device__ __forceinline__ void hist_select_t(ForEach&& for_each, int nr, const int* rk, uint64_t kmin,
+                                              uint64_t kmax, uint64_t* out, Sm& sm) {
+    constexpr int NT = NW * WAVE;
     const int tid = threadIdx.x;
     uint64_t tlo[4], thi[4];
     int tr[4];
@@ -337,7 +338,7 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
         out[t] = kmin;
     }
     bool shrink[4] = {false, false, false, false};
-    // at most 4 groups x 6 levels (11 bits each) are ever needed; the bound only guards
+    // at most 4 groups x 8 levels (>= 8 bits each) are ever needed; the bound only guards
     for (int it = 0; it < 32; ++it) {
         int t0 = -1;
 #pragma unroll
@@ -365,8 +366,8 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
                     }
                 }
             });
-            mn = block_min_u64<SNW>(mn, sm.u64s);
-            mx = block_max_u64<SNW>(mx, sm.u64s + SNW);
+            mn = block_min_u64<NW>(mn, sm.u64s);
+            mx = block_max_u64<NW>(mx, sm.u64s + NW);
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 if (grp[t]) {
@@ -383,8 +384,10 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
             if (mn == mx) continue;   // block-uniform
         }
         const uint64_t span = hi - lo;
-        const int shift = span < (uint64_t)HB ? 0 : 64 - __clzll(span) - 11;   // span >> shift < HB
-        for (int i = tid; i < HB; i += ST) sm.hist[i] = 0u;
+        constexpr int LB = HBN == 2048 ? 11 : HBN == 1024 ? 10 : HBN == 512 ? 9 : 8;
+        static_assert((1 << LB) == HBN, "hist_select: HBN must be 256 .. 2048, a power of two");
+        const int shift = span < (uint64_t)HBN ? 0 : 64 - __clzll(span) - LB;   // span >> shift < HBN
+        for (int i = tid; i < HBN; i += NT) sm.hist[i] = 0u;
         __syncthreads();
         for_each([&](double x) {
             if (!isnan(x)) {
@@ -394,7 +397,7 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
         });
         __syncthreads();
         // block scan: thread tid owns bins [8 tid, 8 tid + 8)
-        constexpr int BPT = HB / ST;
+        constexpr int BPT = HBN / NT;
         uint32_t h[BPT];
         int loc = 0;
 #pragma unroll
@@ -403,7 +406,7 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
             loc += (int)h[j];
         }
         int tot = 0;
-        int run = block_excl_scan<SNW>(loc, sm.ints, &tot);
+        int run = block_excl_scan<NW>(loc, sm.ints, &tot);
 #pragma unroll
         for (int j = 0; j < BPT; ++j) {
 #pragma unroll
@@ -433,7 +436,7 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
             if (blo[t] == bhi[t]) {           // one distinct key in the bin: it is the answer
                 out[t] = blo[t];
                 done[t] = true;
-            } else if (cnt <= HCAP) {         // compact + sort
+            } else if (cnt <= CAP) {         // compact + sort
                 lrank[t] = tr[t] - below;
                 lcnt[t] = cnt;
                 any_list = true;
@@ -476,30 +479,33 @@ __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const in
                 for (int u = 0; u < 4; ++u)
                     if (k >= ulo[u] && k <= uhi[u]) {
                         const uint32_t pos = atomicAdd(&sm.hcnt[u], 1u);
-                        if (pos < (uint32_t)HCAP) sm.buf[u * HCAP + pos] = k;
+                        if (pos < (uint32_t)CAP) sm.buf[u * CAP + pos] = k;
                     }
             }
         });
         __syncthreads();
-        {
-            const int w = tid / WAVE;
-            if (w < nl) {
-                const int c = (int)sm.hcnt[w];
-                uint64_t* L = sm.buf + w * HCAP;
-                if (c <= WAVE) wave_sort_lds<1>(L, c);
-                else if (c <= 2 * WAVE) wave_sort_lds<2>(L, c);
-                else wave_sort_lds<4>(L, c);
-            }
+        for (int w = tid / WAVE; w < nl; w += NW) {   // one wave per list
+            const int c = (int)sm.hcnt[w];
+            uint64_t* L = sm.buf + w * CAP;
+            if (c <= WAVE) wave_sort_lds<1>(L, c);
+            else if (CAP <= 2 * WAVE || c <= 2 * WAVE) wave_sort_lds<(CAP <= 2 * WAVE ? 2 : 2)>(L, c);
+            else wave_sort_lds<(CAP > 2 * WAVE ? 4 : 2)>(L, c);
         }
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             if (lst[t] >= 0) {
-                out[t] = sm.buf[lst[t] * HCAP + lrank[t]];
+                out[t] = sm.buf[lst[t] * CAP + lrank[t]];
                 done[t] = true;
             }
         __syncthreads();   // lists and histogram are reused by the next level / caller
     }
+}
+
+template <typename ForEach>
+__device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const int* rk, uint64_t kmin,
+                                            uint64_t kmax, uint64_t* out, SelSmem& sm) {
+    hist_select_t<SNW, HB, HCAP>(for_each, nr, rk, kmin, kmax, out, sm);
 }
 
 // Number of entries of the ascending list L[0..64) that precede v in the merged order:
@@ -787,6 +793,43 @@ __device__ __forceinline__ void pick_tail(const double* L, int c, int ra, int rb
     };
     va = ra < c ? at(ra) : tau;
     vb = rb < c ? at(rb) : tau;
+}
+
+// pick_tail over the concatenation of two LDS candidate lists L1[0..c1) ++ L2[0..c2)
+template <int R>
+__device__ __forceinline__ void pick_tail2(const double* L1, int c1, const double* L2, int c2, int ra, int rb,
+                                           double tau, double& va, double& vb) {
+    const int lane = lane_id();
+    const int c = c1 + c2;
+    double v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane + WAVE * r;
+        v[r] = e < c1 ? L1[e] : (e < c ? L2[e - c1] : INFINITY);
+    }
+    wave_sort_f64<R>(v);
+    auto at = [&](int e) -> double {
+        double x = v[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r)
+            if ((e >> 6) == r) x = v[r];   // e is wave-uniform
+        return __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(x), e & 63));
+    };
+    va = ra < c ? at(ra) : tau;
+    vb = rb < c ? at(rb) : tau;
+}
+
+// Number of entries of the ascending u32 list L[0..64) below v (inclusive: <= v).
+__device__ __forceinline__ int count_below_u32(const uint32_t* L, uint32_t v, bool inclusive) {
+    int lo = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+        const uint32_t x = L[lo + step - 1];
+        lo += (x < v || (inclusive && x == v)) ? step : 0;
+    }
+    const uint32_t x = L[lo < WAVE ? lo : WAVE - 1];
+    lo += (lo < WAVE && (x < v || (inclusive && x == v))) ? 1 : 0;
+    return lo;
 }
 
 

@@ -45,6 +45,7 @@ class GramArgs(C.Structure):
 
 
 FM_MONTH_MAX_ROWS = 6144
+FM_SELECT_UNIVERSE_MAX_ROWS = 6144
 
 
 class MonthArgs(C.Structure):
@@ -102,6 +103,7 @@ _SIGS = {
     "fm_select_cuts": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _f64, _f64, _i32, _i32,
                               _p, _p, _p, _p, _p, _p]),
     "fm_select": (_i32, [C.POINTER(SelectArgs), _p]),
+    "fm_select_universe": (_i32, [C.POINTER(SelectArgs), _p, _p, _f64, _f64, _p, _p, _p, _p]),
     "fm_clip": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_standardize": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_universe_level": (_i32, [_p, _p, _i32, _i64, _p, _p, _p, _p]),

@@ -81,12 +81,13 @@ def time_launch(tag, reps=20):
     re-issued launches rewrite the same outputs with the same values."""
     name, struct, keep = LAST_LAUNCH[tag]
     st = _stream()
-    L.call(name, L.C.byref(struct), st)
+    args = (L.C.byref(struct),) if struct is not None else keep[1]
+    L.call(name, *args, st)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        L.call(name, L.C.byref(struct), st)
+        L.call(name, *args, st)
     e1.record()
     e1.synchronize()
     return e0.elapsed_time(e1) / reps
@@ -256,6 +257,33 @@ def standardize(panel: DevicePanel, mean, sd, src=None, out=None):
            panel.seg_off.data_ptr(), panel.nseg, panel.nrows, mean.data_ptr(), sd.data_ptr(),
            _stream())
     return out
+
+
+def select_universe(panel: DevicePanel, q_lo, q_hi, min_count, q_a=0.2, q_b=0.5, tag="fm_select_universe"):
+    """Winsorize cuts (+ Gram pivot) of every column AND the NYSE me breakpoints with the
+    universe level byte per row, in one launch (fm_select_universe).  Returns (Cuts,
+    (cut_a, cut_b), level) or None when the months are too long for it."""
+    if panel.max_seg_len > L.FM_SELECT_UNIVERSE_MAX_ROWS or panel.me is None or panel.nyse is None:
+        return None
+    src = panel.cols
+    C, T = src.shape[0], panel.nseg
+    dev = src.device
+    lo = torch.empty((C, T), dtype=torch.float64, device=dev)
+    hi = torch.empty_like(lo)
+    cen = torch.empty_like(lo)
+    nv = torch.empty((C, T), dtype=torch.int32, device=dev)
+    ca = torch.empty(T, dtype=torch.float64, device=dev)
+    cb = torch.empty_like(ca)
+    level = torch.empty(panel.nrows, dtype=torch.uint8, device=dev)
+    sa = L.SelectArgs(cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, seg_off=panel.seg_off.data_ptr(),
+                      nseg=T, max_seg_len=max(panel.max_seg_len, 1), row_mask=None, q_lo=float(q_lo),
+                      q_hi=float(q_hi), min_count=int(min_count), lerp_mode=LERP_NUMPY, lo=lo.data_ptr(),
+                      hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=None, sd=None, center=cen.data_ptr())
+    args = (L.C.byref(sa), panel.me.data_ptr(), panel.nyse.data_ptr(), float(q_a), float(q_b), ca.data_ptr(),
+            cb.data_ptr(), level.data_ptr())
+    _kcall(tag, "fm_select_universe", *args, _stream())
+    LAST_LAUNCH[tag] = ("fm_select_universe", None, (sa, args, src, lo, hi, cen, nv, ca, cb, level, panel))
+    return Cuts(lo, hi, nv, center=cen), (ca, cb), level
 
 
 def nyse_breakpoints(panel: DevicePanel, q_a=0.2, q_b=0.5):

@@ -157,6 +157,14 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
         res, cuts = E.month_pass(panel, models, level=level, nlevels=nlevels, q_lo=cfg.lower_percentile / 100,
                                  q_hi=cfg.upper_percentile / 100, min_count=5, moments=cfg.forecasts)
         return res, names, cuts, level, bp
+    if cfg.universes and cfg.winsorize and not cfg.standardize:
+        # one launch: winsorize cuts of every column + NYSE breakpoints + universe levels
+        r = E.select_universe(panel, cfg.lower_percentile / 100, cfg.upper_percentile / 100, 5)
+        if r is not None:
+            cuts, bp, level = r
+            res = E.fm_pass(panel, models, level=level, nlevels=3, cuts=cuts, shift=cuts.center,
+                            add_back=cuts.center, moments=cfg.forecasts)
+            return res, names, cuts, level, bp
     if cfg.universes:
         side = _side_stream(main.device)
         side.wait_stream(main)
