@@ -84,11 +84,16 @@ def main():
         if world > 1:
             gres = E.FMResult(problems=res.problems, rec=rec_g, status=st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
-        ix, summ, roll, pred, pst = LW.time_series_stage(gres, cfg, moments=res.moments,
-                                                         seg_lo=seg_lo, seg_hi=seg_hi)
+        ix, summ, roll, pred, pst, psumm = LW.time_series_stage(gres, cfg, moments=res.moments,
+                                                                seg_lo=seg_lo, seg_hi=seg_hi)
+        merged[0] = psumm
         return gres, summ, pred, pst
 
+    merged = [None]
+
     def phase_pred(pred, pst):
+        if merged[0] is not None:    # unsharded: summarized inside fm_ts_fused
+            return merged[0]
         psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
         return psumm
 

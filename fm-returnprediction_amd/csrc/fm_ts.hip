@@ -309,7 +309,6 @@ namespace {
 constexpr int FT = 256;
 constexpr int FNW = FT / WAVE;
 constexpr int RROWS = 64;    // rows per rolling workgroup (4 predictive rows per wave pass)
-constexpr int RPIECE = 8;    // rolling outputs per task: one direct window sum, then slides
 constexpr int MAXL = 8;      // Newey-West lags accumulated in one sweep
 
 __host__ __device__ __forceinline__ size_t ts_ix_bytes(int T) { return ((size_t)T * 4 + 15) & ~(size_t)15; }
@@ -420,6 +419,55 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
     }
 }
 
+// The predictive FM summary inside the same launch: every rolling workgroup of problem p
+// arrives on pcounter[p] after its predictive rows are stored (every wave's stores drained,
+// workgroup barrier, one lane's agent-scope release, relaxed agent-scope add); the LAST
+// arriver acquires (agent scope: this CU's L1 is invalidated before any pred row is read),
+// resets the counter for the next launch and summarizes slope, R2 and N over the fitted
+// predictive rows (ts_compact_lds + ts_summary_wg on the predictive records).
+__device__ void ts_pred_arrive(const fm_ts_args& a, int p, double* lds_d) {
+    if (a.pred == nullptr || a.pcounter == nullptr) return;   // block-uniform
+    __shared__ int last;
+    __shared__ int wtot2[FNW];
+    __shared__ double dred2[(MAXL + 1) * FNW];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pred / status stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int nchunk = (a.nseg + RROWS - 1) / RROWS;
+        const uint32_t old = __hip_atomic_fetch_add(a.pcounter + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old + 1u == (uint32_t)nchunk;
+        if (last) {
+            __hip_atomic_store(a.pcounter + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last) return;   // block-uniform
+    fm_ts_args ap = a;
+    ap.rec = a.pred;
+    ap.r_seg = 4;
+    ap.r_prob = (int64_t)a.nseg * 4;
+    ap.status = a.pred_status;
+    ap.s_seg = 1;
+    ap.s_prob = a.nseg;
+    ap.kmax = 3;
+    ap.mean = a.pmean;
+    ap.se = a.pse;
+    ap.tstat = a.ptstat;
+    ap.nobs = a.pnobs;
+    // the workgroup's LDS: [fitted-month list][staging] (ts_fused_kernel's layout)
+    int* ixs = reinterpret_cast<int*>(lds_d - ts_ix_bytes(a.nseg) / 8);
+    double* xs = lds_d;
+    const int cnt = ts_compact_lds(ap, p, ixs, wtot2);
+    for (int k = 0; k < 3; ++k) {
+        ts_summary_wg(ap, p, k, ixs, cnt, xs, wtot2, dred2);
+        __syncthreads();
+    }
+}
+
 __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* ixs, int cnt,
                               double* lds_d) {
     const int tid = threadIdx.x;
@@ -439,7 +487,10 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
                 a.pred_status[(int64_t)p * T + i] = 0;
             }
     }
-    if (r0 >= cnt) return;                               // block-uniform
+    if (r0 >= cnt) {                                     // block-uniform
+        ts_pred_arrive(a, p, lds_d);
+        return;
+    }
     const int r1 = r0 + RROWS < cnt ? r0 + RROWS : cnt;
     const int q0 = predictive ? (r0 - a.lag > 0 ? r0 - a.lag : 0) : r0;   // rows rolled here
     const int j0 = q0 - a.window + 1 > 0 ? q0 - a.window + 1 : 0;          // rows read
@@ -452,39 +503,61 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
         xs[e] = rp[(int64_t)ixs[j0 + j] * a.r_seg + k];
     }
     __syncthreads();
-    const int npc = (nq + RPIECE - 1) / RPIECE;
-    for (int task = tid; task < PM * npc; task += FT) {
-        const int k = task / npc, i0 = q0 + (task - k * npc) * RPIECE;
-        const int i1 = i0 + RPIECE < r1 ? i0 + RPIECE : r1;
+    // per-column inclusive prefix sums of the finite values and their counts over the staged
+    // rows (each output is then a difference of two prefixes: no serial window sums).  A
+    // column's rows are split over 16 threads: local scans, then the 16 block totals.
+    double* ps = rl + nq * PM;                        // [nsrc][PM] prefix sums
+    int* pc = reinterpret_cast<int*>(ps + nsrc * PM);  // [nsrc][PM] prefix counts
+    for (int kb = 0; kb < PM; kb += 16) {
+        const int k = kb + (tid >> 4), part = tid & 15;   // 16 columns x 16 parts at a time
+        const int per = (nsrc + 15) / 16;
+        const int a0 = part * per, a1 = a0 + per < nsrc ? a0 + per : nsrc;
         double sm = 0.0;
-        int c = 0;
-        for (int j = (i0 - a.window + 1 > 0 ? i0 - a.window + 1 : 0); j <= i0; ++j) {
-            const double x = xs[(j - j0) * PM + k];
-            if (isfinite(x)) {
-                sm += x;
-                ++c;
-            }
-        }
-        for (int i = i0; i < i1; ++i) {
-            if (i > i0) {
-                const double x = xs[(i - j0) * PM + k];
-                if (isfinite(x)) {
+        int cn = 0;
+        if (k < PM) {
+            for (int j = a0; j < a1; ++j) {
+                const double x = xs[j * PM + k];
+                if (isfinite(x)) {   // pandas rolling: +-inf -> NaN (Window._prep_values)
                     sm += x;
-                    ++c;
+                    ++cn;
                 }
-                const int jo = i - a.window;
-                if (jo >= 0) {
-                    const double y = xs[(jo - j0) * PM + k];
-                    if (isfinite(y)) {
-                        sm -= y;
-                        --c;
-                    }
-                }
+                ps[j * PM + k] = sm;
+                pc[j * PM + k] = cn;
             }
-            const double m = c >= a.min_periods ? sm / (double)c : NAN;
-            rl[(i - q0) * PM + k] = m;
-            if (i >= r0) a.roll[((int64_t)p * T + i) * PM + k] = m;
         }
+        // exclusive prefix of the 16 part totals (lanes of one 16-lane row group)
+        double bs = sm;
+        int bc = cn;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const double ys = __shfl_up(bs, o, 16);
+            const int yc = __shfl_up(bc, o, 16);
+            if (part >= o) {
+                bs += ys;
+                bc += yc;
+            }
+        }
+        bs -= sm;
+        bc -= cn;
+        if (k < PM)
+            for (int j = a0; j < a1; ++j) {
+                ps[j * PM + k] += bs;
+                pc[j * PM + k] += bc;
+            }
+    }
+    __syncthreads();
+    for (int e = tid; e < nq * PM; e += FT) {
+        const int q = e / PM, k = e - q * PM, i = q0 + q;
+        const int jlo = i - a.window;                 // prefix just before the window
+        double sm = ps[(i - j0) * PM + k];
+        int cn = pc[(i - j0) * PM + k];
+        if (jlo >= j0) {
+            sm -= ps[(jlo - j0) * PM + k];
+            cn -= pc[(jlo - j0) * PM + k];
+        }
+        const double m = cn >= a.min_periods && cn > 0 ? sm / (double)cn : NAN;
+        rl[q * PM + k] = m;
+        if (i >= r0) a.roll[((int64_t)p * T + i) * PM + k] = m;
     }
     if (!predictive) return;
     __syncthreads();
@@ -544,6 +617,7 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
             a.pred_status[(int64_t)p * T + i] = st;
         }
     }
+    ts_pred_arrive(a, p, lds_d);
 }
 
 __global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {
@@ -571,7 +645,9 @@ extern "C" size_t fm_ts_fused_lds_bytes(int32_t nseg, int32_t pmax, int32_t wind
     size_t d = (size_t)nseg * 8;
     if (rolling) {
         const size_t l = predictive ? (size_t)lag : 0;
-        const size_t r = (size_t)pmax * 8 * ((RROWS + l + (size_t)window - 1) + (RROWS + l));
+        const size_t nsrc = RROWS + l + (size_t)window - 1;
+        // staged rows, rolling means, prefix sums (8 B) and prefix counts (4 B)
+        const size_t r = (size_t)pmax * (8 * nsrc + 8 * (RROWS + l) + 12 * nsrc);
         d = d > r ? d : r;
     }
     return ts_ix_bytes(nseg) + d;

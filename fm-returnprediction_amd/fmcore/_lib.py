@@ -72,6 +72,7 @@ class TsArgs(C.Structure):
         ("work", _p), ("window", _i32), ("min_periods", _i32), ("pmax", _i32), ("roll", _p),
         ("moments", _p), ("mom_stride", _i32), ("prob_k", _p), ("lag", _i32), ("seg_lo", _i32),
         ("seg_hi", _i32), ("pred", _p), ("pred_status", _p),
+        ("pmean", _p), ("pse", _p), ("ptstat", _p), ("pnobs", _p), ("pcounter", _p),
     ]
 
 
@@ -128,6 +129,7 @@ _SIGS = {
     "fm_distinct_count": (_i32, [_p, _i64, _p, _i64, _i32, _p, _i32, _i32, _i64, _i64, _p, _p, _p]),
     "fm_firm_chars": (_i32, [C.POINTER(CharsArgs), _p]),
     "fm_rolling_std": (_i32, [_p, _p, _i64, _i32, _i32, _f64, _p, _p]),
+    "fm_rolling_beta": (_i32, [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p]),
     "fm_gen_panel": (_i32, [C.c_uint64, _i64, _i32, _i32, _f64, _f64, _p, _i64, _p, _p, _p]),
     "fm_stream_probe": (_i32, [_p, _i64, _p, _p]),
 }

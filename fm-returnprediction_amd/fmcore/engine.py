@@ -745,7 +745,7 @@ def summarize_predictive(pred, pst, nw_lags=4):
     if not ts_fused_fits(T):
         ix = ts_compact(pst, 1, T, T, P)
         return ts_summary(pred, 4, T * 4, ix, T, P, 3, nw_lags), ix
-    ix, summ, _, _, _ = ts_fused(pred, 4, T * 4, pst, 1, T, T, P, 3, nw_lags)
+    ix, summ, _, _, _, _ = ts_fused(pred, 4, T * 4, pst, 1, T, T, P, 3, nw_lags)
     return summ, ix
 
 
@@ -756,12 +756,27 @@ def ts_fused_fits(nseg, pmax=0, window=None, lag=1, predictive=False):
     return need <= L.FM_TS_FUSED_MAX_LDS
 
 
+_PCOUNTERS = {}
+
+
+def _pcounter(nprob, dev):
+    """Zeroed arrival counters of fm_ts_fused's merged predictive summary (the kernel leaves
+    them zero again), one buffer per (size, device, stream)."""
+    key = (nprob, str(dev), _stream())
+    t = _PCOUNTERS.get(key)
+    if t is None:
+        t = _PCOUNTERS[key] = torch.zeros(nprob, dtype=torch.int32, device=dev)
+    return t
+
+
 def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_lags=4,
              window=None, min_periods=None, pmax=None, moments=None, mom_stride=0, prob_k=None,
-             lag=1, seg_lo=0, seg_hi=None, predictive=False):
+             lag=1, seg_lo=0, seg_hi=None, predictive=False, merge_pred_summary=False):
     """The whole time-series stage in one launch (fm_ts_fused): TSIndex, Summary and, when
     ``window`` is given, the rolling means [P, T, pmax]; with ``predictive`` also the
-    predictive records [P, T, 4] and status [P, T]."""
+    predictive records [P, T, 4] and status [P, T]; with ``merge_pred_summary`` (unsharded
+    runs) also their FM summary, from the same launch.  Returns (ix, summ, roll, pred, pst,
+    psumm or None)."""
     dev = rec.device
     idx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
     cnt = torch.empty(nprob, dtype=torch.int32, device=dev)
@@ -771,25 +786,37 @@ def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_la
     roll = pred = pst = None
     if window is not None:
         roll = torch.empty((nprob, nseg, pmax), dtype=torch.float64, device=dev)
+    psumm = None
+    pc = None
     if predictive:
         pred = torch.empty((nprob, nseg, 4), dtype=torch.float64, device=dev)
         pst = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
+        if merge_pred_summary:
+            pm = torch.empty((nprob, 3), dtype=torch.float64, device=dev)
+            psumm = Summary(pm, torch.empty_like(pm), torch.empty_like(pm),
+                            torch.empty((nprob, 3), dtype=torch.int32, device=dev))
+            pc = _pcounter(nprob, dev)
     ta = L.TsArgs(rec=rec.data_ptr(), r_seg=r_seg, r_prob=r_prob, status=status.data_ptr(), s_seg=s_seg,
                   s_prob=s_prob, nseg=nseg, nprob=nprob, kmax=kmax, nw_lags=nw_lags, idx=idx.data_ptr(),
                   count=cnt.data_ptr(), mean=mean.data_ptr(), se=se.data_ptr(), tstat=ts.data_ptr(),
                   nobs=nobs.data_ptr(), work=None, window=window or 0,
                   min_periods=min_periods or 0, pmax=pmax or 0, roll=_ptr(roll), moments=_ptr(moments),
                   mom_stride=mom_stride, prob_k=_ptr(prob_k), lag=lag, seg_lo=seg_lo,
-                  seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst))
+                  seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst),
+                  pmean=_ptr(psumm.mean if psumm else None), pse=_ptr(psumm.se if psumm else None),
+                  ptstat=_ptr(psumm.tstat if psumm else None), pnobs=_ptr(psumm.nobs if psumm else None),
+                  pcounter=_ptr(pc))
     _kcall("fm_ts_fused", "fm_ts_fused", L.C.byref(ta), _stream())
     _remember("fm_ts_fused", "fm_ts_fused", ta, rec, status, idx, cnt, mean, se, ts, nobs, roll,
-              moments, prob_k, pred, pst)
-    return TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst
+              moments, prob_k, pred, pst, psumm, pc)
+    return TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst, psumm
 
 
 def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag=1, seg_lo=0,
                        seg_hi=None, moments=None, rolling=True, predictive=True):
-    """compact_result + summarize_result + rolling_result + predictive_result in one launch."""
+    """compact_result + summarize_result + rolling_result + predictive_result in one launch;
+    in an unsharded run (all months local) also the predictive FM summary.  Returns (ix,
+    summ, roll, pred, pst, psumm or None: then summarize_predictive after the combine)."""
     T, P, rs = res.rec.shape
     mom = res.moments if moments is None else moments
     window = window if (rolling or predictive) else None
@@ -801,12 +828,14 @@ def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag
             roll = rolling_result(res, ix, window, min_periods)
         if predictive:
             pred, pst = predictive_result(res, ix, roll, lag, seg_lo, seg_hi, moments)
-        return ix, summ, roll, pred, pst
+        return ix, summ, roll, pred, pst, None
     pk = _small_tensor(tuple(p.K for p in res.problems), torch.int32, res.rec.device) if predictive else None
+    unsharded = seg_lo == 0 and (seg_hi is None or seg_hi == T)
     return ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
                     window=window, min_periods=min_periods,
                     pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
-                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive)
+                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive,
+                    merge_pred_summary=predictive and unsharded)
 
 
 def forecast(panel: DevicePanel, coef, cols=None):
@@ -908,6 +937,25 @@ def rolling_std(ids, x, window=252, min_periods=100, scale=252 ** 0.5, out=None)
         raise ValueError("rolling_std: out must be a contiguous float64 [n] tensor")
     _kcall("fm_rolling_std", "fm_rolling_std", ids.data_ptr(), x.data_ptr(), n, int(window),
            int(min_periods), float(scale), out.data_ptr(), _stream())
+    return out
+
+
+def rolling_beta(day, ri, rm, seg_off, q_seg, q_day0, q_day1, period_weeks=156):
+    """fm_rolling_beta on device tensors: day int32 [n], ri / rm float64 [n] (firm-major,
+    days ascending per firm), seg_off int64 [nseg+1]; queries int32 [nq]; -> float64 [nq]."""
+    n = int(day.shape[0])
+    for t, dt in ((day, torch.int32), (ri, torch.float64), (rm, torch.float64), (seg_off, torch.int64),
+                  (q_seg, torch.int32), (q_day0, torch.int32), (q_day1, torch.int32)):
+        if t.dtype != dt or t.dim() != 1 or not t.is_contiguous():
+            raise ValueError(f"rolling_beta: expected contiguous {dt} vectors")
+    if ri.shape[0] != n or rm.shape[0] != n:
+        raise ValueError("rolling_beta: day / ri / rm lengths differ")
+    nq = int(q_seg.shape[0])
+    out = torch.empty(nq, dtype=torch.float64, device=day.device)
+    ws = torch.empty((5, max(n, 1)), dtype=torch.float64, device=day.device)
+    _kcall("fm_rolling_beta", "fm_rolling_beta", day.data_ptr(), ri.data_ptr(), rm.data_ptr(), n,
+           seg_off.data_ptr(), int(seg_off.shape[0]) - 1, int(period_weeks) * 7, q_seg.data_ptr(),
+           q_day0.data_ptr(), q_day1.data_ptr(), nq, ws.data_ptr(), out.data_ptr(), _stream())
     return out
 
 

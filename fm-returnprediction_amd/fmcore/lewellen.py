@@ -199,20 +199,19 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
 
 
 def time_series_stage(res: E.FMResult, cfg: PipelineConfig, moments=None, seg_lo=0, seg_hi=None):
-    # one launch (fm_ts_fused): compaction, FM summaries, rolling means, predictive slopes
-    ix, summ, roll, pred, pst = E.time_series_result(
+    """One launch (fm_ts_fused): compaction, FM summaries, rolling means, predictive slopes
+    and, unsharded, their FM summary.  Returns (ix, summ, roll, pred, pst, psumm or None)."""
+    return E.time_series_result(
         res, cfg.nw_lags, cfg.window, cfg.min_periods, cfg.lag, seg_lo=seg_lo, seg_hi=seg_hi,
         moments=moments, rolling=cfg.forecasts or cfg.fig1, predictive=cfg.forecasts)
-    return ix, summ, roll, pred, pst
 
 
 def run_pipeline(panel: E.DevicePanel, cfg: PipelineConfig = None, model_cols=None, y="retx"):
     cfg = cfg or PipelineConfig()
     model_cols = model_cols or table2_models()
     res, names, cuts, level, bp = local_stage(panel, cfg, model_cols, y)
-    ix, summ, roll, pred, pst = time_series_stage(res, cfg)
-    psumm = None
-    if cfg.forecasts:
+    ix, summ, roll, pred, pst, psumm = time_series_stage(res, cfg)
+    if cfg.forecasts and psumm is None:
         psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
     return PipelineResult(model_names=names, model_cols=dict(model_cols, **({"Figure 1": FIG1_VARS} if cfg.fig1 else {})),
                           res=res, ix=ix, summary=summ, rolling=roll, pred=pred, pred_status=pst,

@@ -16,8 +16,9 @@ Firm-axis characteristic builders (§8(f) row 2; one fused device pass, fm_firm_
   calc_log_issues_36, calc_debt_price, calc_sales_price   reference :137-341
   calc_std_12      reference :438-466   252-day rolling std on device (fm_rolling_std)
   calc_characteristics (extension): all twelve monthly characteristics in one launch.
-Data pulls, the polars weekly beta (calculate_rolling_beta, :344-435) and LaTeX output of
-the reference are outside this drop-in (scope).
+  calculate_rolling_beta reference :344-434  polars 156-week weekly-window beta on device
+                   (fm_rolling_beta; parity unpinned: no polars here)
+Data pulls and LaTeX output of the reference are outside this drop-in (scope).
 """
 import os
 import sys
@@ -268,6 +269,44 @@ def calc_characteristics(crsp_comp: pd.DataFrame, names=None) -> pd.DataFrame:
     for nm in names:
         crsp_comp[nm] = out[nm]
     return crsp_comp
+
+
+def calculate_rolling_beta(crsp_d: pd.DataFrame, crsp_index_d: pd.DataFrame,
+                           crsp_comp: pd.DataFrame) -> pd.DataFrame:
+    """156-week rolling market beta from daily log returns, merged onto crsp_comp as `beta`
+    (reference src/calc_Lewellen_2014.py:344-434).  The reference's polars
+    group_by_dynamic(every="1w", period="156w", by="permno") windows, sums and beta formula
+    run on device (fm_rolling_beta); the inner join on the date, the (permno, date) sort
+    and the final left merge on (permno, jdate) are the reference's pandas steps.  Parity
+    unpinned: polars is not installed here (oracle/chars_oracle.py restates its semantics)."""
+    import torch
+    dev = _E.require_device()
+    df = crsp_d[["permno", "dlycaldt", "retx"]].rename(columns={"retx": "Ri", "dlycaldt": "date"})
+    mkt = crsp_index_d[["caldt", "vwretx"]].rename(columns={"vwretx": "Rm", "caldt": "date"})
+    j = df.merge(mkt, on="date", how="inner").sort_values(["permno", "date"], kind="stable")
+    permno = j["permno"].to_numpy()
+    days = j["date"].values.astype("datetime64[D]").astype(np.int64)
+    if len(days) and (days.min() < -(2 ** 31) or days.max() >= 2 ** 31):
+        raise ValueError("calculate_rolling_beta: dates out of range")
+    starts = np.flatnonzero(np.r_[True, permno[1:] != permno[:-1]]) if len(permno) else np.zeros(0, np.int64)
+    seg_off = np.r_[starts, len(permno)].astype(np.int64)
+    uperm = permno[starts]
+    keys = crsp_comp[["permno", "jdate"]].drop_duplicates()
+    kp = keys["permno"].to_numpy()
+    pos = np.searchsorted(uperm, kp) if len(uperm) else np.zeros(len(kp), dtype=np.int64)
+    ok = pos < len(uperm)
+    ok[ok] = uperm[pos[ok]] == kp[ok]
+    kq = keys.loc[ok]
+    per = pd.to_datetime(kq["jdate"]).dt.to_period("M")
+    d0 = per.dt.start_time.values.astype("datetime64[D]").astype(np.int64)
+    d1 = per.dt.end_time.values.astype("datetime64[D]").astype(np.int64)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    beta = _E.rolling_beta(t(days, np.int32), t(j["Ri"].to_numpy(dtype=np.float64), np.float64),
+                           t(j["Rm"].to_numpy(dtype=np.float64), np.float64), t(seg_off, np.int64),
+                           t(pos[ok], np.int32), t(d0, np.int32), t(d1, np.int32)).cpu().numpy()
+    # a (permno, month) without an emitted window is NaN after the merge either way
+    right = kq.assign(beta=beta)
+    return pd.merge(left=crsp_comp, right=right[["permno", "jdate", "beta"]], on=["permno", "jdate"], how="left")
 
 
 def calc_std_12(crsp_d: pd.DataFrame, crsp_comp: pd.DataFrame) -> pd.DataFrame:

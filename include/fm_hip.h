@@ -43,6 +43,8 @@
  *                      calc_sales_price (src/calc_Lewellen_2014.py:137-341, called at :537-548)
  *   fm_rolling_std  <- calc_std_12's groupby("permno")["retx"].rolling(252,
  *                      min_periods=100).std() * sqrt(252) (src/calc_Lewellen_2014.py:448-456)
+ *   fm_rolling_beta <- calculate_rolling_beta's polars 156-week group_by_dynamic beta
+ *                      (src/calc_Lewellen_2014.py:344-434)
  *   fm_gen_panel    <- (bench/test data) counter-based synthetic panel, bit-identical to
  *                      fmcore/synth.py
  *
@@ -285,6 +287,15 @@ typedef struct fm_ts_args {
     int32_t lag, seg_lo, seg_hi;
     double* pred;                 /* [nprob][nseg][4] or NULL */
     uint32_t* pred_status;        /* [nprob][nseg] */
+    /* optional (unsharded runs): the FM summary of the predictive records (slope, R2, N:
+     * kmax 3) computed in the same launch by the last rolling workgroup of each problem
+     * (agent-scope release / acquire on pcounter).  pcounter [nprob] must be zero on entry
+     * and is zero again on exit; NULL = no merged summary (call fm_ts_fused on pred). */
+    double* pmean;                /* [nprob][3] */
+    double* pse;
+    double* ptstat;
+    int32_t* pnobs;
+    uint32_t* pcounter;
 } fm_ts_args;
 
 /* LDS bytes the fused launch stages per workgroup; it must not exceed FM_TS_FUSED_MAX_LDS
@@ -358,6 +369,20 @@ int fm_firm_chars(const fm_chars_args* args, void* stream);
  * (a std needs at least 2 observations, so min_periods 1 behaves as 2). */
 int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, int32_t window,
                    int32_t min_periods, double scale, double* out, void* stream);
+
+/* calculate_rolling_beta's 156-week rolling market beta (src/calc_Lewellen_2014.py:344-434,
+ * polars group_by_dynamic(every="1w", period="156w", by="permno"), closed left, label left,
+ * windows from the Monday of each firm's first date while the start <= its last date,
+ * empty windows not emitted).  Rows: the inner join of daily stock and market returns,
+ * firm-major (seg_off[nseg+1] firm row ranges), days ascending within a firm (`day` =
+ * days since 1970-01-01); ri / rm the raw daily returns (log(1 + r) is taken here).  Query
+ * q = (firm segment q_seg, calendar month [q_day0, q_day1]): the beta of the LAST emitted
+ * window starting in that month, NaN if none (the reference's drop_duplicates(keep="last")
+ * + left merge, :426-431).  ws: [5][n] workspace.  Parity unpinned (no polars here). */
+int fm_rolling_beta(const int32_t* day, const double* ri, const double* rm, int64_t n,
+                    const int64_t* seg_off, int32_t nseg, int32_t period_days,
+                    const int32_t* q_seg, const int32_t* q_day0, const int32_t* q_day1,
+                    int32_t nq, double* ws, double* beta, void* stream);
 
 int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
                  double nan_rate, double nyse_rate, double* cols, int64_t col_stride,

@@ -134,3 +134,76 @@ def std_12_merge(d_permno, d_dates, d_std, m_permno, m_jdate):
         last[(int(p), int(j))] = s
     mj = np.asarray(m_jdate).astype("datetime64[ns]").astype(np.int64)
     return np.array([last.get((int(p), int(j)), np.nan) for p, j in zip(np.asarray(m_permno), mj)])
+
+
+# ----------------------------------------------------------------------------------------
+# calculate_rolling_beta (src/calc_Lewellen_2014.py:344-434) -- PARITY UNPINNED: the
+# reference computes it with polars (pinned polars==1.22.0, requirements.txt:36), which is
+# not installed here, so no golden from the reference exists.  Restated from the polars
+# semantics the reference code relies on:
+#   * inner join of the daily stock rows with the daily market index on the date (:375);
+#     log_Ri = log(1 + Ri), log_Rm = log(1 + Rm) (:379-382); sorted by (permno, date);
+#   * group_by_dynamic(index_column="date", every="1w", period="156w", by="permno") with
+#     polars 1.x defaults: offset 0, closed="left", label="left", start_by="window": per
+#     permno, windows [S, S + 156 weeks) for the Mondays S from the week of the first date
+#     (dt.truncate("1w") = Monday) while S <= the last date; a window with no rows is not
+#     emitted; the row's `date` is S (:393-401);
+#   * sums of log_Ri, log_Rm, log_Ri * log_Rm, log_Rm ** 2 and the row count; polars float
+#     sums propagate NaN (the pandas -> polars constructor keeps NaN as NaN, not null);
+#     beta = (sum_RiRm - sum_Ri * sum_Rm / N) / (sum_Rm2 - sum_Rm ** 2 / N) (:402-416);
+#   * jdate = month end of S; drop_duplicates(["permno", "jdate"], keep="last") -- the LAST
+#     window starting in that month -- then a left merge onto crsp_comp (:426-431).
+# ----------------------------------------------------------------------------------------
+WEEK = 7
+
+
+def week_start(days):
+    """polars dt.truncate('1w') on day numbers since 1970-01-01 (a Thursday): Monday."""
+    days = np.asarray(days, dtype=np.int64)
+    return days - np.mod(days + 3, WEEK)
+
+
+def rolling_beta_windows(permno, days, lri, lrm, period_weeks=156):
+    """All emitted windows: (permno, window start day, beta).  Rows sorted by (permno, day)."""
+    permno = np.asarray(permno)
+    days = np.asarray(days, dtype=np.int64)
+    out_p, out_s, out_b = [], [], []
+    bounds = np.flatnonzero(np.r_[True, permno[1:] != permno[:-1], True])
+    span = period_weeks * WEEK
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        d = days[a:b]
+        x, y = lri[a:b], lrm[a:b]
+        S = int(week_start(d[:1])[0])
+        while S <= d[-1]:
+            i0 = np.searchsorted(d, S, side="left")
+            i1 = np.searchsorted(d, S + span, side="left")
+            if i1 > i0:
+                xs, ys = x[i0:i1], y[i0:i1]
+                n = float(i1 - i0)
+                with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+                    s_ri, s_rm = xs.sum(), ys.sum()
+                    num = (xs * ys).sum() - s_ri * s_rm / n
+                    den = (ys ** 2).sum() - s_rm ** 2 / n
+                    out_b.append(num / den)
+                out_p.append(permno[a])
+                out_s.append(S)
+            S += WEEK
+    return np.array(out_p), np.array(out_s, dtype=np.int64), np.array(out_b, dtype=np.float64)
+
+
+def calculate_rolling_beta(crsp_d, crsp_index_d, crsp_comp, period_weeks=156):
+    """The reference's calculate_rolling_beta restated (see the block comment above)."""
+    df = crsp_d[["permno", "dlycaldt", "retx"]].rename(columns={"retx": "Ri", "dlycaldt": "date"})
+    mkt = crsp_index_d[["caldt", "vwretx"]].rename(columns={"vwretx": "Rm", "caldt": "date"})
+    j = df.merge(mkt, on="date", how="inner")
+    with np.errstate(invalid="ignore", divide="ignore"):
+        j["lri"] = np.log(j["Ri"].to_numpy(dtype=np.float64) + 1.0)
+        j["lrm"] = np.log(j["Rm"].to_numpy(dtype=np.float64) + 1.0)
+    j = j.sort_values(["permno", "date"], kind="stable")
+    days = j["date"].values.astype("datetime64[D]").astype(np.int64)
+    p, s, b = rolling_beta_windows(j["permno"].to_numpy(), days, j["lri"].to_numpy(),
+                                   j["lrm"].to_numpy(), period_weeks)
+    beta = pd.DataFrame({"permno": p, "date": s.astype("datetime64[D]").astype("datetime64[ns]"), "beta": b})
+    beta["jdate"] = beta["date"].dt.to_period("M").dt.to_timestamp("M")
+    beta = beta.drop_duplicates(subset=["permno", "jdate"], keep="last")
+    return pd.merge(left=crsp_comp, right=beta[["permno", "jdate", "beta"]], on=["permno", "jdate"], how="left")

@@ -94,3 +94,38 @@ def chars_inputs(g):
     d = pd.DataFrame({"permno": g["din_permno"], "dlycaldt": g["din_dlycaldt"].astype("datetime64[ns]"),
                       "retx": g["din_retx"]}, index=pd.Index(g["din_index"]))
     return m, d
+
+
+def beta_inputs(seed=3, nfirms=30):
+    """Synthetic daily stock / market returns and a monthly (permno, jdate) frame for the
+    156-week rolling beta (tests only): ragged firm date ranges over business days, a firm
+    with a > 3-year gap (empty weekly windows), NaN returns, a -100% return (log -> -inf),
+    market index days missing (the inner join drops them), months outside every firm's
+    range and a permno with no daily data."""
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    bdays = pd.bdate_range("1990-01-01", "2001-12-31")
+    mkt_days = bdays[rng.random(len(bdays)) > 0.01]
+    rm = rng.normal(0.0004, 0.01, len(mkt_days))
+    crsp_index_d = pd.DataFrame({"caldt": mkt_days, "vwretx": rm})
+    rows = []
+    for f in range(nfirms):
+        a = int(rng.integers(0, len(bdays) - 300))
+        b = int(rng.integers(a + 50, len(bdays)))
+        d = bdays[a:b]
+        if f == 3:   # a gap longer than the 156-week window
+            d = d[(d < bdays[a] + pd.Timedelta(days=200)) | (d > bdays[a] + pd.Timedelta(days=1500))]
+        beta = rng.normal(1.0, 0.4)
+        m = np.interp(d.values.astype("int64"), mkt_days.values.astype("int64"), rm)
+        r = beta * m + rng.normal(0, 0.015, len(d))
+        if f in (7, 8):
+            r[rng.random(len(d)) < 0.002] = np.nan
+        if f == 5:
+            r[len(r) // 2] = -1.0
+        rows.append(pd.DataFrame({"permno": 10000 + f, "dlycaldt": d, "retx": r}))
+    crsp_d = pd.concat(rows, ignore_index=True).sample(frac=1.0, random_state=seed).reset_index(drop=True)
+    months = pd.date_range("1989-06-30", "2002-06-30", freq="ME")
+    comp = [(10000 + f, m) for f in range(nfirms + 1) for m in months[rng.random(len(months)) < 0.7]]
+    crsp_comp = pd.DataFrame(comp, columns=["permno", "jdate"])
+    crsp_comp["mthcaldt"] = crsp_comp["jdate"]
+    return crsp_d, crsp_index_d, crsp_comp

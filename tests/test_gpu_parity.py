@@ -579,7 +579,7 @@ def test_sharded_pipeline_bit_identical(E):
     for (s0, s1), loc in zip(bounds, locs):
         g = E.FMResult(problems=loc.problems, rec=rec, status=st, pmax=loc.pmax, moments=loc.moments,
                        mom_stride=loc.mom_stride)
-        ix, summ, roll, p, ps = LW.time_series_stage(g, cfg, moments=loc.moments, seg_lo=s0, seg_hi=s1)
+        ix, summ, roll, p, ps, _ = LW.time_series_stage(g, cfg, moments=loc.moments, seg_lo=s0, seg_hi=s1)
         for x, y in ((summ.mean, full.summary.mean), (summ.tstat, full.summary.tstat), (roll, full.rolling),
                      (ix.count, full.ix.count)):
             assert _same(x.cpu().numpy(), y.cpu().numpy())
@@ -624,7 +624,7 @@ def test_table1_golden(CL):
 
 # ---------------------------------------------------------------- firm-axis characteristics
 from oracle import chars_oracle as CO  # noqa: E402
-from fmtol import chars_inputs  # noqa: E402
+from fmtol import beta_inputs, chars_inputs  # noqa: E402
 
 _CHAR_FUNCS = ["calc_log_size", "calc_log_bm", "calc_return_12_2", "calc_accruals", "calc_roa",
                "calc_log_assets_growth", "calc_dy", "calc_log_return_13_36", "calc_log_issues_12",
@@ -770,3 +770,17 @@ def test_panel_from_arrow_matches_frame_path(E):
     a1, b1 = E.nyse_breakpoints(got)
     a2, b2 = E.nyse_breakpoints(exp)
     assert _same(a1.cpu().numpy(), a2.cpu().numpy()) and _same(b1.cpu().numpy(), b2.cpu().numpy())
+
+
+def test_rolling_beta_vs_oracle(CL):
+    """§8(f) row 2's 156-week rolling beta (calculate_rolling_beta, reference :344-434) on
+    device against the oracle's restatement of polars group_by_dynamic (parity UNPINNED vs
+    the reference: polars is not installed).  Ragged firms, a > 3-year gap (empty windows),
+    NaN and -100% returns, missing market days, a permno without daily data."""
+    crsp_d, idx, comp = beta_inputs()
+    got = CL.calculate_rolling_beta(crsp_d, idx, comp)
+    exp = CO.calculate_rolling_beta(crsp_d, idx, comp)
+    assert list(got.columns) == list(exp.columns) and len(got) == len(exp)
+    assert np.array_equal(got["permno"].values, exp["permno"].values)
+    assert np.isfinite(exp["beta"].values).sum() > 1000
+    assert_series_close(got["beta"].values, exp["beta"].values, "beta")
