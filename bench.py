@@ -84,16 +84,11 @@ def main():
         if world > 1:
             gres = E.FMResult(problems=res.problems, rec=rec_g, status=st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
-        ix, summ, roll, pred, pst, psumm = LW.time_series_stage(gres, cfg, moments=res.moments,
-                                                                seg_lo=seg_lo, seg_hi=seg_hi)
-        merged[0] = psumm
+        ix, summ, roll, pred, pst = LW.time_series_stage(gres, cfg, moments=res.moments,
+                                                         seg_lo=seg_lo, seg_hi=seg_hi)
         return gres, summ, pred, pst
 
-    merged = [None]
-
     def phase_pred(pred, pst):
-        if merged[0] is not None:    # unsharded: summarized inside fm_ts_fused
-            return merged[0]
         psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
         return psumm
 
@@ -194,16 +189,14 @@ def main():
     for tag in timer.names():
         kern[tag] = timer.avg_ms(tag)   # events around each eager launch (incl. launch gaps)
     fused = "fm_month_pass" in E.LAST_LAUNCH
-    tags = (("fm_month_pass",) if fused else ("fm_select_universe", "fm_select_cuts", "fm_gram")) + \
-        ("fm_select_cuts[nyse]", "fm_solve", "fm_ts_fused")
+    tags = (("fm_month_pass",) if fused else ("fm_select_cuts", "fm_gram")) + \
+        ("fm_select_cuts[nyse]", "fm_solve", "fm_ts_fused", "fm_ts_fused[pred]")
     dev_ms = {t: E.time_launch(t) for t in tags if t in E.LAST_LAUNCH}
     # algorithmic HBM bytes per launch: every panel column once (8 B per
     # value), the universe level byte, and the month tables written (cuts, pivots, Gram
     # partials); fm_select alone reads the columns only
     T_l = panel.nseg
-    cand = {"fm_select_cuts": rows_local * C * 8, "fm_gram": rows_local * (C * 8 + 1),
-            # every column + me + the NYSE flag read, the level byte written
-            "fm_select_universe": rows_local * (C * 8 + 8 + 1 + 1)}
+    cand = {"fm_select_cuts": rows_local * C * 8, "fm_gram": rows_local * (C * 8 + 1)}
     if fused:
         partial = E.LAST_LAUNCH["fm_month_pass"][2][2]          # [T, buckets, 136] Gram partials
         cand["fm_month_pass"] = rows_local * (C * 8 + 1) + T_l * C * (3 * 8 + 4) + partial.numel() * 8

@@ -13,8 +13,9 @@
 //   beta_query_kernel   one thread per (firm, month) query: the last Monday S of the month
 //                       inside [week(first date), last date] whose window holds a row
 //                       (binary searches on the firm's days), window sums as prefix
-//                       differences; a window with a non-finite log return is summed
-//                       directly in row order (IEEE NaN / inf propagation as in polars)
+//                       differences; a window of <= 128 rows or with a non-finite log
+//                       return is summed directly (IEEE NaN / inf propagation as in
+//                       polars; a one-row window's 0/0 stays NaN)
 #include <math.h>
 
 #include "fm_common.h"
@@ -90,6 +91,57 @@ __device__ __forceinline__ int64_t lower_bound_days(const int32_t* day, int64_t 
     return lo;
 }
 
+// numpy's pairwise-sum leaf (a block of <= 128 values: eight running accumulators combined
+// as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the n % 8 tail; < 8 values in order), so a
+// short window's sums are the oracle's bit for bit.  Longer windows (non-finite ones only)
+// are summed in row order: NaN / inf propagate the same either way.
+constexpr int PW_BLOCK = 128;
+
+__device__ __forceinline__ void window_sums(const double* ri, const double* rm, int64_t i0, int64_t i1,
+                                            double s[5]) {
+    const int64_t n = i1 - i0;
+    auto at = [&](int64_t i, double v[4]) {
+        const double x = log(ri[i] + 1.0), y = log(rm[i] + 1.0);
+        v[0] = x;
+        v[1] = y;
+        v[2] = x * y;
+        v[3] = y * y;
+    };
+    double v[4];
+    if (n < 8 || n > PW_BLOCK) {
+        s[0] = s[1] = s[2] = s[3] = 0.0;
+        for (int64_t i = i0; i < i1; ++i) {
+            at(i, v);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s[k] += v[k];
+        }
+        return;
+    }
+    double r[4][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        at(i0 + j, v);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k][j] = v[k];
+    }
+    const int64_t m = n - n % 8;
+    for (int64_t i = 8; i < m; i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            at(i0 + i + j, v);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k][j] += v[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] = ((r[k][0] + r[k][1]) + (r[k][2] + r[k][3])) + ((r[k][4] + r[k][5]) + (r[k][6] + r[k][7]));
+    for (int64_t i = m; i < n; ++i) {
+        at(i0 + i, v);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] += v[k];
+    }
+}
+
 __global__ __launch_bounds__(BT) void beta_query_kernel(const int32_t* __restrict__ day,
                                                         const double* __restrict__ ri,
                                                         const double* __restrict__ rm,
@@ -114,15 +166,10 @@ __global__ __launch_bounds__(BT) void beta_query_kernel(const int32_t* __restric
 #pragma unroll
             for (int k = 0; k < 5; ++k)
                 s[k] = ws[(int64_t)k * n + i1 - 1] - (i0 > a ? ws[(int64_t)k * n + i0 - 1] : 0.0);
-            if (s[4] > 0.0) {   // a non-finite log return: sum the window directly (IEEE)
-                s[0] = s[1] = s[2] = s[3] = 0.0;
-                for (int64_t i = i0; i < i1; ++i) {
-                    const double x = log(ri[i] + 1.0), y = log(rm[i] + 1.0);
-                    s[0] += x;
-                    s[1] += y;
-                    s[2] += x * y;
-                    s[3] += y * y;
-                }
+            if (s[4] > 0.0 || i1 - i0 <= PW_BLOCK) {
+                // short windows (prefix differences lose digits there, and a one-row window
+                // must give 0/0) and windows with a non-finite log return: summed directly
+                window_sums(ri, rm, i0, i1, s);
             }
             const double N = (double)(i1 - i0);
             beta = (s[2] - s[0] * s[1] / N) / (s[3] - s[1] * s[1] / N);

@@ -271,73 +271,33 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
 //      unit's loads are issued here;
 //   4. wave 0 sorts the two low-tail lists together and reads ranks i0, j0; wave 1 the high
 //      tail.
-// A unit the tail path cannot decide (ranks >= 128, candidate overflow) is finished in the
-// same workgroup by the adaptive histogram select on the register values (hist_select_t),
-// so no fallback launch follows.  With universes (PairArgs::me), the first nseg units are
-// the months' NYSE `me` breakpoints (pandas lerp, nyse row mask: hist_select_t) and the
-// workgroup then writes the month's universe level bytes from the same registers, which
-// replaces the separate breakpoint / level launches of get_subsets.
-struct PairArgs {
-    SelArgs a;
-    const double* me;      // [rows] or NULL (no universe units)
-    const uint8_t* nyse;   // [rows]
-    double qa, qb;         // pandas quantiles (0.2, 0.5)
-    double* cut_a;         // [nseg]
-    double* cut_b;
-    uint8_t* level;        // [rows]
-};
-
-constexpr int PHB = 1024;   // pair kernel hist_select: bins
-constexpr int PCAP = 128;   // pair kernel hist_select: keys per list
-
+// A unit the tail path cannot decide (ranks >= 128, candidate overflow: rare for 1/99
+// cuts) is marked (nvalid = -1) and redone by the workgroup kernel's fallback pass.  Keeping
+// the histogram select out of this kernel keeps its register count (the values are held in
+// registers) at the level the hot path needs.
 struct PairSmem {
-    union {
-        struct {
-            uint32_t sk[2][2][WAVE];   // [wave][lo / hi][lane] sorted high words
-            double ext[2][2][WAVE];    // [wave][min / max][lane] lane extrema
-            double cand[2][2][WCAP];   // [wave][lo / hi] tail candidates
-        };
-        struct {
-            uint32_t hist[PHB];
-            uint64_t buf[4 * PCAP];
-        };
-    };
+    uint32_t sk[2][2][WAVE];   // [wave][lo / hi][lane] sorted high words
+    double ext[2][2][WAVE];    // [wave][min / max][lane] lane extrema
+    double cand[2][2][WCAP];   // [wave][lo / hi] tail candidates
     int ni[2][4];
     double tv[2];
     double res[2];
     int okv[2];
-    int hs[12];
-    uint32_t hcnt[4];
-    int ints[8];
-    uint64_t u64s[4];
 };
 
 template <int VPH>
-__global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(PairArgs pa) {
-    const SelArgs& a = pa.a;
+__global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
     __shared__ PairSmem sm;
     const int lane = lane_id();
     const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
-    const int nuni = pa.me ? a.nseg : 0;             // universe units first (the slow ones)
-    const int64_t nunits = (int64_t)a.nseg * a.ncols + nuni;
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
     int64_t k = blockIdx.x;
     if (k >= nunits) return;   // block-uniform
     double xv[VPH];
-    uint64_t mbits = ~0ull;    // universe units: NYSE row bits of this thread's values
-    int s_cur = 0;
     auto load = [&](int64_t kk) -> int {
-        int s, c;
-        const double* base;
-        if (kk < nuni) {
-            s = (int)kk;
-            c = 0;
-            base = pa.me;
-        } else {
-            const int64_t u = unit_of(a, kk - nuni);
-            s = (int)(u % a.nseg);
-            c = (int)(u / a.nseg);
-            base = a.cols + (int64_t)c * a.col_stride;
-        }
+        const int64_t u = unit_of(a, kk);
+        const int s = (int)(u % a.nseg), c = (int)(u / a.nseg);
+        const double* base = a.cols + (int64_t)c * a.col_stride;
         const int64_t r0 = a.seg_off[s];
         const int L = (int)(a.seg_off[s + 1] - r0);
         typedef const __attribute__((address_space(1))) char* gptr;
@@ -354,43 +314,19 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(PairArgs pa) {
     };
     int L = load(k);
     while (true) {
-        const bool uni = k < nuni;   // block-uniform
-        int s = 0, c = 0;
-        int64_t u = 0;
-        if (uni) {
-            s = (int)k;
-        } else {
-            u = unit_of(a, k - nuni);
-            s = (int)(u % a.nseg);
-            c = (int)(u / a.nseg);
-        }
-        (void)c;
+        const int64_t u = unit_of(a, k);
         const int64_t kn = k + gridDim.x;
         const bool more = kn < nunits;
         int Ln = 0;
         int row0 = h * WAVE + lane;
         asm volatile("" : "+v"(row0));
-        mbits = ~0ull;
-        if (uni) {
-            // NYSE rows of this thread's values (row (2v + h) * 64 + lane of the month)
-            const uint8_t* nb = pa.nyse + a.seg_off[s];
-            mbits = 0;
-            if (L > 0) {
-#pragma unroll
-                for (int v = 0; v < VPH; ++v) {
-                    const int r = row0 + v * 2 * WAVE;
-                    const bool in = nb[r < L ? r : L - 1] != 0 && r < L;
-                    mbits |= (uint64_t)in << v;
-                }
-            }
-        }
         // ---- 1. this wave's half: count, lane extrema (NaN = absent / masked out)
         int nh = 0;
         double mn4[4] = {NAN, NAN, NAN, NAN}, mx4[4] = {NAN, NAN, NAN, NAN};
 #pragma unroll
         for (int v = 0; v < VPH; ++v) {
             if (row0 + v * 2 * WAVE >= L) xv[v] = NAN;   // past the segment end
-            const double x = (mbits >> v) & 1 ? xv[v] : NAN;
+            const double x = xv[v];
             nh += (int)__popcll(__ballot(!isnan(x)));
             mn4[v & 3] = hw_min(mn4[v & 3], x);
             mx4[v & 3] = hw_max(mx4[v & 3], x);
@@ -398,11 +334,10 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(PairArgs pa) {
         const double mn = hw_min(hw_min(mn4[0], mn4[1]), hw_min(mn4[2], mn4[3]));
         const double mx = hw_max(hw_max(mx4[0], mx4[1]), hw_max(mx4[2], mx4[3]));
         nh = __builtin_amdgcn_readfirstlane(nh);
-        const double q_lo = uni ? pa.qa : a.q_lo, q_hi = uni ? pa.qb : a.q_hi;
-        const int mode = uni ? 1 : a.lerp_mode;
-        const int minc = uni ? 1 : a.min_count;
-        bool fast = !uni;
-        if (fast) {
+        const double q_lo = a.q_lo, q_hi = a.q_hi;
+        const int mode = a.lerp_mode;
+        const int minc = a.min_count;
+        {
             const uint32_t ha = isnan(mn) ? 0xFFFFFFFFu : (uint32_t)(dkey(mn) >> 32);
             const uint32_t hb = isnan(mx) ? 0xFFFFFFFFu : (uint32_t)(~dkey(mx) >> 32);
             uint32_t ta[1] = {ha}, tb[1] = {hb};
@@ -423,7 +358,7 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(PairArgs pa) {
             qranks(n, q_lo, mode, i0, j0, g0);
             qranks(n, q_hi, mode, i1, j1, g1);
         }
-        bool ok = fast && apply;
+        bool ok = apply;
         if (ok) {
             // ---- 2. this wave's tail: h == 0 low (rank j0 over lane minima), h == 1 high
             const int kr = h == 0 ? j0 : n - 1 - i1;
@@ -503,42 +438,8 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(PairArgs pa) {
             hi = sm.res[1];
         }
         if (apply && !ok) {
-            // ---- exact adaptive histogram select on the register values: universe units
-            // (middle ranks) and the rare tails the path above cannot decide
-            uint64_t kmn = SENT, kmx = 0;
-#pragma unroll
-            for (int v = 0; v < VPH; ++v) {
-                const double x = (mbits >> v) & 1 ? xv[v] : NAN;
-                if (!isnan(x)) {
-                    const uint64_t kk = dkey(x);
-                    kmn = kk < kmn ? kk : kmn;
-                    kmx = kk > kmx ? kk : kmx;
-                }
-            }
-            __syncthreads();   // the fast path's LDS (aliased by the histogram) is dead
-            kmn = block_min_u64<2>(kmn, sm.u64s);
-            kmx = block_max_u64<2>(kmx, sm.u64s + 2);
-            const int rk[4] = {i0, j0, i1, j1};
-            uint64_t ko[4];
-            hist_select_t<2, PHB, PCAP>([&](auto&& f) {
-#pragma unroll
-                for (int v = 0; v < VPH; ++v) f((mbits >> v) & 1 ? xv[v] : NAN);
-            }, 4, rk, kmn, kmx, ko, sm);
-            lo = qlerp(kval(ko[0]), kval(ko[1]), g0, mode);
-            hi = qlerp(kval(ko[2]), kval(ko[3]), g1, mode);
-        }
-        if (uni) {
-            // me_20 / me_50 and the month's universe levels (NaN me or cut: comparison false)
-            if (threadIdx.x == 0) {
-                pa.cut_a[s] = lo;
-                pa.cut_b[s] = hi;
-            }
-            uint8_t* lv = pa.level + a.seg_off[s];
-#pragma unroll
-            for (int v = 0; v < VPH; ++v) {
-                const int r = row0 + v * 2 * WAVE;
-                if (r < L) lv[r] = (uint8_t)((xv[v] >= lo ? 1 : 0) + (xv[v] >= hi ? 1 : 0));
-            }
+            // redone by the workgroup kernel's fallback pass
+            if (threadIdx.x == 0) a.nvalid[u] = -1;
         } else if (h == 0) {
             double cen = 0.5 * (lo + hi);
             if (!isfinite(cen)) {
@@ -578,7 +479,7 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(PairArgs pa) {
         }
         if (more) Ln = load(kn);   // xv is dead: the next unit's loads fly across the barrier
         __syncthreads();
-        if (!uni && a.center && !isfinite(0.5 * (lo + hi)) && threadIdx.x == 0) {
+        if ((ok || !apply) && a.center && !isfinite(0.5 * (lo + hi)) && threadIdx.x == 0) {
             // pivot fallback: the midpoint of the finite range (both halves), else 0
             const double m1 = hw_min(sm.res[0], sm.tv[0]), m2 = hw_max(sm.res[1], sm.tv[1]);
             double cen = 0.5 * (m1 + m2);
@@ -605,7 +506,7 @@ int select_wave_grid(int64_t nunits) {
 }
 
 template <int VPH>
-void launch_select_pair(const PairArgs& a, hipStream_t st) {
+void launch_select_pair(const SelArgs& a, hipStream_t st) {
     static int ncu = [] {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -613,20 +514,20 @@ void launch_select_pair(const PairArgs& a, hipStream_t st) {
             n = 256;
         return n;
     }();
-    const int64_t nunits = (int64_t)a.a.nseg * a.a.ncols + (a.me ? a.a.nseg : 0);
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
     const int64_t cap = (int64_t)ncu * 8;   // eight 2-wave workgroups per CU (4 waves / SIMD)
     hipLaunchKernelGGL((select_pair_kernel<VPH>), dim3((unsigned)(nunits < cap ? nunits : cap)), dim3(2 * WAVE),
                        0, st, a);
 }
 
-int launch_select_pair_vph(const PairArgs& pa, int max_seg_len, hipStream_t st) {
+int launch_select_pair_vph(const SelArgs& a, int max_seg_len, hipStream_t st) {
     const int vph = (max_seg_len + 2 * WAVE - 1) / (2 * WAVE);
-    if (vph <= 8) launch_select_pair<8>(pa, st);
-    else if (vph <= 16) launch_select_pair<16>(pa, st);
-    else if (vph <= 24) launch_select_pair<24>(pa, st);
-    else if (vph <= 32) launch_select_pair<32>(pa, st);
-    else if (vph <= 40) launch_select_pair<40>(pa, st);
-    else if (vph <= 48) launch_select_pair<48>(pa, st);
+    if (vph <= 8) launch_select_pair<8>(a, st);
+    else if (vph <= 16) launch_select_pair<16>(a, st);
+    else if (vph <= 24) launch_select_pair<24>(a, st);
+    else if (vph <= 32) launch_select_pair<32>(a, st);
+    else if (vph <= 40) launch_select_pair<40>(a, st);
+    else if (vph <= 48) launch_select_pair<48>(a, st);
     else {
         set_error("select pair kernel: %d-row segments exceed %d", max_seg_len, 48 * 2 * WAVE);
         return FM_ETOOBIG;
@@ -654,36 +555,6 @@ void launch_select_wave(const SelArgs& a, hipStream_t st) {
 
 }  // namespace
 }  // namespace fm
-
-extern "C" int fm_select_universe(const fm_select_args* args, const double* me, const uint8_t* nyse,
-                                  double q_a, double q_b, double* cut_a, double* cut_b, uint8_t* level,
-                                  void* stream) {
-    using namespace fm;
-    FM_REQUIRE(args != nullptr, "fm_select_universe: null args");
-    const fm_select_args& x = *args;
-    FM_REQUIRE(x.cols && x.seg_off && x.lo && x.hi && x.nvalid && me && nyse && cut_a && cut_b && level,
-               "fm_select_universe: null pointer");
-    FM_REQUIRE(x.ncols > 0 && x.ncols <= 65535 && x.nseg >= 0, "fm_select_universe: bad sizes");
-    FM_REQUIRE(x.row_mask == nullptr && x.mean == nullptr && x.sd == nullptr,
-               "fm_select_universe: no row mask / moments (use fm_select)");
-    FM_REQUIRE(x.lerp_mode == 0 || x.lerp_mode == 1, "fm_select_universe: lerp_mode must be 0 or 1");
-    FM_REQUIRE(x.q_lo >= 0.0 && x.q_lo <= 1.0 && x.q_hi >= 0.0 && x.q_hi <= 1.0 && q_a >= 0.0 && q_a <= 1.0 &&
-                   q_b >= 0.0 && q_b <= 1.0,
-               "fm_select_universe: quantiles must be in [0,1]");
-    if (x.max_seg_len > FM_SELECT_UNIVERSE_MAX_ROWS) {
-        set_error("fm_select_universe: %d-row months exceed %d (use fm_select + fm_universe_level)",
-                  x.max_seg_len, FM_SELECT_UNIVERSE_MAX_ROWS);
-        return FM_ETOOBIG;
-    }
-    if (x.nseg == 0) return FM_OK;
-    SelArgs a{x.cols,        x.col_stride, x.seg_off, x.nseg,    x.ncols, nullptr, x.q_lo, x.q_hi,
-              x.min_count, x.lerp_mode,  x.lo,      x.hi,      x.nvalid, nullptr, nullptr, x.center};
-    PairArgs pa{a, me, nyse, q_a, q_b, cut_a, cut_b, level};
-    const int rc = launch_select_pair_vph(pa, x.max_seg_len > 0 ? x.max_seg_len : 1, (hipStream_t)stream);
-    if (rc != FM_OK) return rc;
-    FM_CHECK_LAUNCH("fm_select_universe");
-    return FM_OK;
-}
 
 extern "C" int fm_select_cuts(const double* cols, int64_t col_stride, int32_t ncols,
                               const int64_t* seg_off, int32_t nseg, int32_t max_seg_len,
@@ -731,13 +602,10 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
 #endif
     (void)vpl;
     if (wave && x.mean == nullptr && vpl <= 96 && !getenv_flag_one_wave()) {
-        // two waves per unit (the common Table-2 case: no moments), self-contained: no
-        // fallback launch follows
-        PairArgs pa{a, nullptr, nullptr, 0.0, 0.0, nullptr, nullptr, nullptr};
-        const int rc = launch_select_pair_vph(pa, max_seg_len, st);
+        // two waves per unit (the common Table-2 case: no moments)
+        const int rc = launch_select_pair_vph(a, max_seg_len, st);
         if (rc != FM_OK) return rc;
         FM_CHECK_LAUNCH("fm_select_cuts(pair)");
-        return FM_OK;
     } else if (wave) {
         if (vpl <= 16) launch_select_wave<16>(a, st);
         else if (vpl <= 32) launch_select_wave<32>(a, st);

@@ -8,8 +8,8 @@
 // by a Cholesky factorization (one wavefront per problem, lanes over matrix entries).
 // When a pivot collapses (1 - R^2 of a regressor on the previous ones <= 1e-9, e.g. an
 // all-zero column or an exactly collinear pair) the wave falls back to a Jacobi
-// eigen-decomposition of Sxx and the minimum-norm (pseudo-inverse) solution, which is
-// what statsmodels' pinv returns when the null space does not involve the intercept.
+// eigen-decomposition of Sxx and the minimum-norm (pseudo-inverse) solution of the
+// uncentered design [1, X] (what statsmodels' pinv returns, see jacobi_pinv).
 // R^2 = 1 - (Syy - b'Sxy)/Syy (centered TSS: the model has a constant).
 //
 // One workgroup (4 waves) per month: the month's bucket Grams are first summed over its
@@ -43,9 +43,17 @@ struct WaveScratch {
     double sxy[MD], sdiag[MD], mu[MD], b[MD];
 };
 
-// Cyclic Jacobi + pseudo-inverse solve by lane 0 (rare fallback path).
+// Cyclic Jacobi + pseudo-inverse solve by lane 0 (rare fallback path).  A = Sxx (centered),
+// mur[0..K-1] = the regressors' raw means and mur[K] = y's.  The range part is the centered
+// minimum-norm slope vector b_c; statsmodels' pinv minimizes over the UNCENTERED design
+// [1, X] instead, whose null space also holds every affine dependence (a regressor constant
+// within the month, x2 = a x1 + c): with N = the null eigenvectors of Sxx, w = N' mur and
+// beta0_c = ybar - b_c' mur, the min-norm LS solution is
+//     b = b_c + N w beta0_c / (1 + |w|^2),  beta0 = beta0_c / (1 + |w|^2)
+// (minimize beta0^2 + |b|^2 over b = b_c + N t, beta0 = beta0_c - w' t).  The intercept is
+// then ybar - b' mur as on the regular path, which equals the beta0 above.
 template <int MD>
-__device__ void jacobi_pinv(double* A, double* V, int K, const double* sxy, double* b) {
+__device__ void jacobi_pinv(double* A, double* V, int K, const double* sxy, const double* mur, double* b) {
     for (int i = 0; i < K; ++i)
         for (int j = 0; j < K; ++j) V[i * MD + j] = i == j ? 1.0 : 0.0;
     double frob = 0.0;
@@ -93,6 +101,22 @@ __device__ void jacobi_pinv(double* A, double* V, int K, const double* sxy, doub
         for (int k = 0; k < K; ++k) proj += V[k * MD + i] * sxy[k];
         proj /= l;
         for (int j = 0; j < K; ++j) b[j] += proj * V[j * MD + i];
+    }
+    double b0 = mur[K], den = 1.0;
+    for (int j = 0; j < K; ++j) b0 -= b[j] * mur[j];
+    for (int i = 0; i < K; ++i) {
+        if (A[i * MD + i] > EIG_REL * lmax) continue;
+        double wi = 0.0;
+        for (int k = 0; k < K; ++k) wi += V[k * MD + i] * mur[k];
+        den += wi * wi;
+    }
+    if (!(den > 1.0) || !isfinite(b0)) return;   // the null space misses the intercept
+    for (int i = 0; i < K; ++i) {
+        if (A[i * MD + i] > EIG_REL * lmax) continue;
+        double wi = 0.0;
+        for (int k = 0; k < K; ++k) wi += V[k * MD + i] * mur[k];
+        const double t = b0 * wi / den;
+        for (int j = 0; j < K; ++j) b[j] += t * V[j * MD + i];
     }
 }
 
@@ -276,8 +300,9 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
             for (int j = 0; j < MD; ++j)
                 if (j < K && lane < K) ws.A[lane * MD + j] = Gp[li * MD + 1 + j] - g0 * Gp[1 + j] / n;
             if (lane < K) ws.sxy[lane] = sxy;
+            if (lane < K1) ws.mu[lane] = mu + (a.add_back ? a.add_back[(int64_t)(zl - 1) * a.nseg + s] : 0.0);
             wave_sync();
-            if (lane == 0) jacobi_pinv<MD>(ws.A, ws.V, K, ws.sxy, ws.b);
+            if (lane == 0) jacobi_pinv<MD>(ws.A, ws.V, K, ws.sxy, ws.mu, ws.b);
             wave_sync();
             bi = lane < K ? ws.b[lane] : 0.0;
             wave_sync();
@@ -500,9 +525,11 @@ __global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
                         if (c < Kq) J.A[(i - 1) * 16 + c] = G[c + 1] - G[0] * g0c[c] / nq;
                     J.sxy[i - 1] = sxy;
                 }
+                if (g == gq && i >= 1 && i <= Kq + 1)   // raw means of x_0..x_{K-1}, y
+                    J.mu[i - 1] = mu + (a.add_back ? a.add_back[(int64_t)(zi - 1) * a.nseg + s] : 0.0);
             }
             wave_sync();
-            if (lane == 0) jacobi_pinv<16>(J.A, J.V, Kq, J.sxy, J.b);
+            if (lane == 0) jacobi_pinv<16>(J.A, J.V, Kq, J.sxy, J.mu, J.b);
             wave_sync();
             if (g == gq && i >= 1 && i <= Kq) bi = J.b[i - 1];
             wave_sync();

@@ -419,55 +419,6 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
     }
 }
 
-// The predictive FM summary inside the same launch: every rolling workgroup of problem p
-// arrives on pcounter[p] after its predictive rows are stored (every wave's stores drained,
-// workgroup barrier, one lane's agent-scope release, relaxed agent-scope add); the LAST
-// arriver acquires (agent scope: this CU's L1 is invalidated before any pred row is read),
-// resets the counter for the next launch and summarizes slope, R2 and N over the fitted
-// predictive rows (ts_compact_lds + ts_summary_wg on the predictive records).
-__device__ void ts_pred_arrive(const fm_ts_args& a, int p, double* lds_d) {
-    if (a.pred == nullptr || a.pcounter == nullptr) return;   // block-uniform
-    __shared__ int last;
-    __shared__ int wtot2[FNW];
-    __shared__ double dred2[(MAXL + 1) * FNW];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pred / status stores
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int nchunk = (a.nseg + RROWS - 1) / RROWS;
-        const uint32_t old = __hip_atomic_fetch_add(a.pcounter + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old + 1u == (uint32_t)nchunk;
-        if (last) {
-            __hip_atomic_store(a.pcounter + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    __syncthreads();
-    if (!last) return;   // block-uniform
-    fm_ts_args ap = a;
-    ap.rec = a.pred;
-    ap.r_seg = 4;
-    ap.r_prob = (int64_t)a.nseg * 4;
-    ap.status = a.pred_status;
-    ap.s_seg = 1;
-    ap.s_prob = a.nseg;
-    ap.kmax = 3;
-    ap.mean = a.pmean;
-    ap.se = a.pse;
-    ap.tstat = a.ptstat;
-    ap.nobs = a.pnobs;
-    // the workgroup's LDS: [fitted-month list][staging] (ts_fused_kernel's layout)
-    int* ixs = reinterpret_cast<int*>(lds_d - ts_ix_bytes(a.nseg) / 8);
-    double* xs = lds_d;
-    const int cnt = ts_compact_lds(ap, p, ixs, wtot2);
-    for (int k = 0; k < 3; ++k) {
-        ts_summary_wg(ap, p, k, ixs, cnt, xs, wtot2, dred2);
-        __syncthreads();
-    }
-}
-
 __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* ixs, int cnt,
                               double* lds_d) {
     const int tid = threadIdx.x;
@@ -487,10 +438,7 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
                 a.pred_status[(int64_t)p * T + i] = 0;
             }
     }
-    if (r0 >= cnt) {                                     // block-uniform
-        ts_pred_arrive(a, p, lds_d);
-        return;
-    }
+    if (r0 >= cnt) return;                               // block-uniform
     const int r1 = r0 + RROWS < cnt ? r0 + RROWS : cnt;
     const int q0 = predictive ? (r0 - a.lag > 0 ? r0 - a.lag : 0) : r0;   // rows rolled here
     const int j0 = q0 - a.window + 1 > 0 ? q0 - a.window + 1 : 0;          // rows read
@@ -617,7 +565,6 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
             a.pred_status[(int64_t)p * T + i] = st;
         }
     }
-    ts_pred_arrive(a, p, lds_d);
 }
 
 __global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {

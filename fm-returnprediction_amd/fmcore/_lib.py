@@ -45,7 +45,6 @@ class GramArgs(C.Structure):
 
 
 FM_MONTH_MAX_ROWS = 6144
-FM_SELECT_UNIVERSE_MAX_ROWS = 6144
 
 
 class MonthArgs(C.Structure):
@@ -72,7 +71,6 @@ class TsArgs(C.Structure):
         ("work", _p), ("window", _i32), ("min_periods", _i32), ("pmax", _i32), ("roll", _p),
         ("moments", _p), ("mom_stride", _i32), ("prob_k", _p), ("lag", _i32), ("seg_lo", _i32),
         ("seg_hi", _i32), ("pred", _p), ("pred_status", _p),
-        ("pmean", _p), ("pse", _p), ("ptstat", _p), ("pnobs", _p), ("pcounter", _p),
     ]
 
 
@@ -104,7 +102,6 @@ _SIGS = {
     "fm_select_cuts": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _f64, _f64, _i32, _i32,
                               _p, _p, _p, _p, _p, _p]),
     "fm_select": (_i32, [C.POINTER(SelectArgs), _p]),
-    "fm_select_universe": (_i32, [C.POINTER(SelectArgs), _p, _p, _f64, _f64, _p, _p, _p, _p]),
     "fm_clip": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_standardize": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_universe_level": (_i32, [_p, _p, _i32, _i64, _p, _p, _p, _p]),

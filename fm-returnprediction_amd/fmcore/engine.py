@@ -259,33 +259,6 @@ def standardize(panel: DevicePanel, mean, sd, src=None, out=None):
     return out
 
 
-def select_universe(panel: DevicePanel, q_lo, q_hi, min_count, q_a=0.2, q_b=0.5, tag="fm_select_universe"):
-    """Winsorize cuts (+ Gram pivot) of every column AND the NYSE me breakpoints with the
-    universe level byte per row, in one launch (fm_select_universe).  Returns (Cuts,
-    (cut_a, cut_b), level) or None when the months are too long for it."""
-    if panel.max_seg_len > L.FM_SELECT_UNIVERSE_MAX_ROWS or panel.me is None or panel.nyse is None:
-        return None
-    src = panel.cols
-    C, T = src.shape[0], panel.nseg
-    dev = src.device
-    lo = torch.empty((C, T), dtype=torch.float64, device=dev)
-    hi = torch.empty_like(lo)
-    cen = torch.empty_like(lo)
-    nv = torch.empty((C, T), dtype=torch.int32, device=dev)
-    ca = torch.empty(T, dtype=torch.float64, device=dev)
-    cb = torch.empty_like(ca)
-    level = torch.empty(panel.nrows, dtype=torch.uint8, device=dev)
-    sa = L.SelectArgs(cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, seg_off=panel.seg_off.data_ptr(),
-                      nseg=T, max_seg_len=max(panel.max_seg_len, 1), row_mask=None, q_lo=float(q_lo),
-                      q_hi=float(q_hi), min_count=int(min_count), lerp_mode=LERP_NUMPY, lo=lo.data_ptr(),
-                      hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=None, sd=None, center=cen.data_ptr())
-    args = (L.C.byref(sa), panel.me.data_ptr(), panel.nyse.data_ptr(), float(q_a), float(q_b), ca.data_ptr(),
-            cb.data_ptr(), level.data_ptr())
-    _kcall(tag, "fm_select_universe", *args, _stream())
-    LAST_LAUNCH[tag] = ("fm_select_universe", None, (sa, args, src, lo, hi, cen, nv, ca, cb, level, panel))
-    return Cuts(lo, hi, nv, center=cen), (ca, cb), level
-
-
 def nyse_breakpoints(panel: DevicePanel, q_a=0.2, q_b=0.5):
     """me_20 / me_50 per month over NYSE rows (pandas groupby.quantile lerp)."""
     cuts = select_cuts(panel, q_a, q_b, 1, LERP_PANDAS, cols=panel.me.view(1, -1), row_mask=panel.nyse,
@@ -745,7 +718,7 @@ def summarize_predictive(pred, pst, nw_lags=4):
     if not ts_fused_fits(T):
         ix = ts_compact(pst, 1, T, T, P)
         return ts_summary(pred, 4, T * 4, ix, T, P, 3, nw_lags), ix
-    ix, summ, _, _, _, _ = ts_fused(pred, 4, T * 4, pst, 1, T, T, P, 3, nw_lags)
+    ix, summ, _, _, _ = ts_fused(pred, 4, T * 4, pst, 1, T, T, P, 3, nw_lags, tag="fm_ts_fused[pred]")
     return summ, ix
 
 
@@ -756,27 +729,12 @@ def ts_fused_fits(nseg, pmax=0, window=None, lag=1, predictive=False):
     return need <= L.FM_TS_FUSED_MAX_LDS
 
 
-_PCOUNTERS = {}
-
-
-def _pcounter(nprob, dev):
-    """Zeroed arrival counters of fm_ts_fused's merged predictive summary (the kernel leaves
-    them zero again), one buffer per (size, device, stream)."""
-    key = (nprob, str(dev), _stream())
-    t = _PCOUNTERS.get(key)
-    if t is None:
-        t = _PCOUNTERS[key] = torch.zeros(nprob, dtype=torch.int32, device=dev)
-    return t
-
-
 def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_lags=4,
              window=None, min_periods=None, pmax=None, moments=None, mom_stride=0, prob_k=None,
-             lag=1, seg_lo=0, seg_hi=None, predictive=False, merge_pred_summary=False):
+             lag=1, seg_lo=0, seg_hi=None, predictive=False, tag="fm_ts_fused"):
     """The whole time-series stage in one launch (fm_ts_fused): TSIndex, Summary and, when
     ``window`` is given, the rolling means [P, T, pmax]; with ``predictive`` also the
-    predictive records [P, T, 4] and status [P, T]; with ``merge_pred_summary`` (unsharded
-    runs) also their FM summary, from the same launch.  Returns (ix, summ, roll, pred, pst,
-    psumm or None)."""
+    predictive records [P, T, 4] and status [P, T].  Returns (ix, summ, roll, pred, pst)."""
     dev = rec.device
     idx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
     cnt = torch.empty(nprob, dtype=torch.int32, device=dev)
@@ -786,37 +744,26 @@ def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_la
     roll = pred = pst = None
     if window is not None:
         roll = torch.empty((nprob, nseg, pmax), dtype=torch.float64, device=dev)
-    psumm = None
-    pc = None
     if predictive:
         pred = torch.empty((nprob, nseg, 4), dtype=torch.float64, device=dev)
         pst = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
-        if merge_pred_summary:
-            pm = torch.empty((nprob, 3), dtype=torch.float64, device=dev)
-            psumm = Summary(pm, torch.empty_like(pm), torch.empty_like(pm),
-                            torch.empty((nprob, 3), dtype=torch.int32, device=dev))
-            pc = _pcounter(nprob, dev)
     ta = L.TsArgs(rec=rec.data_ptr(), r_seg=r_seg, r_prob=r_prob, status=status.data_ptr(), s_seg=s_seg,
                   s_prob=s_prob, nseg=nseg, nprob=nprob, kmax=kmax, nw_lags=nw_lags, idx=idx.data_ptr(),
                   count=cnt.data_ptr(), mean=mean.data_ptr(), se=se.data_ptr(), tstat=ts.data_ptr(),
                   nobs=nobs.data_ptr(), work=None, window=window or 0,
                   min_periods=min_periods or 0, pmax=pmax or 0, roll=_ptr(roll), moments=_ptr(moments),
                   mom_stride=mom_stride, prob_k=_ptr(prob_k), lag=lag, seg_lo=seg_lo,
-                  seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst),
-                  pmean=_ptr(psumm.mean if psumm else None), pse=_ptr(psumm.se if psumm else None),
-                  ptstat=_ptr(psumm.tstat if psumm else None), pnobs=_ptr(psumm.nobs if psumm else None),
-                  pcounter=_ptr(pc))
-    _kcall("fm_ts_fused", "fm_ts_fused", L.C.byref(ta), _stream())
-    _remember("fm_ts_fused", "fm_ts_fused", ta, rec, status, idx, cnt, mean, se, ts, nobs, roll,
-              moments, prob_k, pred, pst, psumm, pc)
-    return TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst, psumm
+                  seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst))
+    _kcall(tag, "fm_ts_fused", L.C.byref(ta), _stream())
+    _remember(tag, "fm_ts_fused", ta, rec, status, idx, cnt, mean, se, ts, nobs, roll,
+              moments, prob_k, pred, pst)
+    return TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst
 
 
 def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag=1, seg_lo=0,
                        seg_hi=None, moments=None, rolling=True, predictive=True):
-    """compact_result + summarize_result + rolling_result + predictive_result in one launch;
-    in an unsharded run (all months local) also the predictive FM summary.  Returns (ix,
-    summ, roll, pred, pst, psumm or None: then summarize_predictive after the combine)."""
+    """compact_result + summarize_result + rolling_result + predictive_result in one launch.
+    Returns (ix, summ, roll, pred, pst)."""
     T, P, rs = res.rec.shape
     mom = res.moments if moments is None else moments
     window = window if (rolling or predictive) else None
@@ -828,14 +775,12 @@ def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag
             roll = rolling_result(res, ix, window, min_periods)
         if predictive:
             pred, pst = predictive_result(res, ix, roll, lag, seg_lo, seg_hi, moments)
-        return ix, summ, roll, pred, pst, None
+        return ix, summ, roll, pred, pst
     pk = _small_tensor(tuple(p.K for p in res.problems), torch.int32, res.rec.device) if predictive else None
-    unsharded = seg_lo == 0 and (seg_hi is None or seg_hi == T)
     return ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
                     window=window, min_periods=min_periods,
                     pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
-                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive,
-                    merge_pred_summary=predictive and unsharded)
+                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive)
 
 
 def forecast(panel: DevicePanel, coef, cols=None):

@@ -157,14 +157,6 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
         res, cuts = E.month_pass(panel, models, level=level, nlevels=nlevels, q_lo=cfg.lower_percentile / 100,
                                  q_hi=cfg.upper_percentile / 100, min_count=5, moments=cfg.forecasts)
         return res, names, cuts, level, bp
-    if cfg.universes and cfg.winsorize and not cfg.standardize:
-        # one launch: winsorize cuts of every column + NYSE breakpoints + universe levels
-        r = E.select_universe(panel, cfg.lower_percentile / 100, cfg.upper_percentile / 100, 5)
-        if r is not None:
-            cuts, bp, level = r
-            res = E.fm_pass(panel, models, level=level, nlevels=3, cuts=cuts, shift=cuts.center,
-                            add_back=cuts.center, moments=cfg.forecasts)
-            return res, names, cuts, level, bp
     if cfg.universes:
         side = _side_stream(main.device)
         side.wait_stream(main)
@@ -200,7 +192,7 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
 
 def time_series_stage(res: E.FMResult, cfg: PipelineConfig, moments=None, seg_lo=0, seg_hi=None):
     """One launch (fm_ts_fused): compaction, FM summaries, rolling means, predictive slopes
-    and, unsharded, their FM summary.  Returns (ix, summ, roll, pred, pst, psumm or None)."""
+    (their FM summary follows in summarize_predictive).  Returns (ix, summ, roll, pred, pst)."""
     return E.time_series_result(
         res, cfg.nw_lags, cfg.window, cfg.min_periods, cfg.lag, seg_lo=seg_lo, seg_hi=seg_hi,
         moments=moments, rolling=cfg.forecasts or cfg.fig1, predictive=cfg.forecasts)
@@ -210,8 +202,9 @@ def run_pipeline(panel: E.DevicePanel, cfg: PipelineConfig = None, model_cols=No
     cfg = cfg or PipelineConfig()
     model_cols = model_cols or table2_models()
     res, names, cuts, level, bp = local_stage(panel, cfg, model_cols, y)
-    ix, summ, roll, pred, pst, psumm = time_series_stage(res, cfg)
-    if cfg.forecasts and psumm is None:
+    ix, summ, roll, pred, pst = time_series_stage(res, cfg)
+    psumm = None
+    if cfg.forecasts:
         psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
     return PipelineResult(model_names=names, model_cols=dict(model_cols, **({"Figure 1": FIG1_VARS} if cfg.fig1 else {})),
                           res=res, ix=ix, summary=summ, rolling=roll, pred=pred, pred_status=pst,

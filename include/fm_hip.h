@@ -171,19 +171,6 @@ typedef struct fm_select_args {
 
 int fm_select(const fm_select_args* args, void* stream);
 
-/* fm_select_universe: the Table-2 winsorize cuts of fm_select (no row mask, no moments;
- * nvalid required) AND get_subsets' NYSE me breakpoints with the universe level byte per
- * row, in ONE launch (two waves per unit; the months' breakpoint units run first).
- * Replaces np.percentile(vals, 1/99) per month per var (src/calc_Lewellen_2014.py:519-523),
- * groupby("mthcaldt")["me"].quantile([q_a, q_b]) over NYSE rows (:74-82, pandas lerp) and
- * the me >= me_20 / me >= me_50 masks (:95-96): cut_a / cut_b [nseg], level [rows] =
- * (me >= cut_a) + (me >= cut_b), NaN comparisons false.  Months of at most
- * FM_SELECT_UNIVERSE_MAX_ROWS rows, else FM_ETOOBIG (use fm_select + fm_universe_level). */
-#define FM_SELECT_UNIVERSE_MAX_ROWS 6144
-int fm_select_universe(const fm_select_args* args, const double* me, const uint8_t* nyse,
-                       double q_a, double q_b, double* cut_a, double* cut_b, uint8_t* level,
-                       void* stream);
-
 int fm_clip(const double* src, double* dst, int64_t col_stride, int32_t ncols,
             const int64_t* seg_off, int32_t nseg, int64_t nrows,
             const double* lo, const double* hi, void* stream);
@@ -287,15 +274,6 @@ typedef struct fm_ts_args {
     int32_t lag, seg_lo, seg_hi;
     double* pred;                 /* [nprob][nseg][4] or NULL */
     uint32_t* pred_status;        /* [nprob][nseg] */
-    /* optional (unsharded runs): the FM summary of the predictive records (slope, R2, N:
-     * kmax 3) computed in the same launch by the last rolling workgroup of each problem
-     * (agent-scope release / acquire on pcounter).  pcounter [nprob] must be zero on entry
-     * and is zero again on exit; NULL = no merged summary (call fm_ts_fused on pred). */
-    double* pmean;                /* [nprob][3] */
-    double* pse;
-    double* ptstat;
-    int32_t* pnobs;
-    uint32_t* pcounter;
 } fm_ts_args;
 
 /* LDS bytes the fused launch stages per workgroup; it must not exceed FM_TS_FUSED_MAX_LDS

@@ -52,6 +52,11 @@ def assert_series_close(a, b, what="", rtol=RTOL, scale=None):
             with np.errstate(invalid="ignore"):
                 i = int(np.nanargmax(d)) if np.isfinite(d).any() else 0
             msg += f"; worst |diff|={d.flat[i]!r} at {i}: {a.flat[i]!r} vs {b.flat[i]!r}"
+            bad = np.flatnonzero((np.isnan(a) != np.isnan(b)).ravel() |
+                                 (np.isinf(b) & (a != b)).ravel())
+            if bad.size:
+                j = int(bad[0])
+                msg += f"; {bad.size} NaN/inf mismatches, first at {j}: {a.flat[j]!r} vs {b.flat[j]!r}"
         raise AssertionError(msg)
 
 

@@ -103,6 +103,18 @@ def fig1_panel():
     return synth.synth_frame(150, 60, 303, nan_rate=0.02, present_rate=0.97)
 
 
+def fig1_const_panel():
+    """fig1_panel with Figure-1 regressors constant within a month (has_constant='add': the
+    pinv splits the intercept over [1, c1, c2], reference src/calc_Lewellen_2014.py:913-921)
+    -- one month with one nonzero constant, one with two."""
+    df = fig1_panel()
+    m = np.sort(df.mthcaldt.unique())
+    df.loc[df.mthcaldt == m[40], FIG1_VARS[1]] = 0.8
+    df.loc[df.mthcaldt == m[100], FIG1_VARS[0]] = -0.3
+    df.loc[df.mthcaldt == m[100], FIG1_VARS[2]] = 1.7
+    return df
+
+
 def mid_panel():
     return synth.synth_frame(600, 500, 404, nan_rate=0.02, present_rate=0.97)
 
@@ -159,6 +171,23 @@ def edge_cases():
     out.append(("k1", df, ["x0"]))
     df = _edge_base(12, 60, 15, 10)
     out.append(("k15", df, [f"x{k}" for k in range(15)]))
+    return out
+
+
+def divergence_cases():
+    """Rank-deficiency cases beyond edge_cases (DESIGN.md §2 'Known divergences'): an affine
+    dependence x2 = 2 x1 + 0.5 (the pinv null space involves the intercept) in every month,
+    and a near-collinear pair x2 = x1 + 1e-7 noise (sigma_min / sigma_max ~ 1e-7)."""
+    out = []
+    K = 3
+    xs = [f"x{k}" for k in range(K)]
+    df = _edge_base(12, 15, K, 21)
+    df["x2"] = 2.0 * df["x1"] + 0.5
+    out.append(("affine_collinear", df, xs))
+    df = _edge_base(12, 40, K, 22)
+    rng = np.random.default_rng(23)
+    df["x2"] = df["x1"] + 1e-7 * rng.standard_normal(len(df))
+    out.append(("near_collinear", df, xs))
     return out
 
 

@@ -193,8 +193,8 @@ def gen_fm():
     json.dump(meta, open(os.path.join(HERE, "fm.json"), "w"), indent=1)
 
 
-def gen_fig1():
-    df = cases.fig1_panel()
+def gen_fig1(df=None, out="fig1.npz"):
+    df = cases.fig1_panel() if df is None else df
     plt_obj, sm_obj = RecordingPlt(), RecordingSM()
     ns = load_calc(plt_obj, sm_obj)
     w = ns["winsorize"](df, cases.WINSOR_VARS, 1, 99)
@@ -220,7 +220,7 @@ def gen_fig1():
         ax = plt_obj.axes[si]
         d[tag + "|rolling_plotted"] = np.stack([ln[1] for ln in ax.lines], axis=1)
         d[tag + "|plot_x"] = np.asarray(ax.lines[0][0]).astype("datetime64[ns]").astype(np.int64)
-    np.savez_compressed(os.path.join(HERE, "fig1.npz"), **d)
+    np.savez_compressed(os.path.join(HERE, out), **d)
 
 
 def gen_mid():
@@ -240,9 +240,9 @@ def gen_mid():
     json.dump(meta, open(os.path.join(HERE, "mid.json"), "w"), indent=1)
 
 
-def gen_edge():
+def gen_edge(case_list=None, out="edge"):
     d, meta = {}, {}
-    for name, df, xs in cases.edge_cases():
+    for name, df, xs in (cases.edge_cases() if case_list is None else case_list):
         d.update(frame_arrays(df, name + "|in_"))
         try:
             res = R.run_monthly_cs_regressions(df, "retx", xs, "mthcaldt")
@@ -256,8 +256,8 @@ def gen_edge():
                 meta[name]["summary_error"] = type(e).__name__
         except Exception as e:
             meta[name] = {"error": type(e).__name__, "message": str(e)}
-    np.savez_compressed(os.path.join(HERE, "edge.npz"), **d)
-    json.dump(meta, open(os.path.join(HERE, "edge.json"), "w"), indent=1)
+    np.savez_compressed(os.path.join(HERE, out + ".npz"), **d)
+    json.dump(meta, open(os.path.join(HERE, out + ".json"), "w"), indent=1)
 
 
 def gen_nw():
@@ -372,6 +372,8 @@ if __name__ == "__main__":
     gen_wins()
     gen_fm()
     gen_fig1()
+    gen_fig1(cases.fig1_const_panel(), "fig1c.npz")
+    gen_edge(cases.divergence_cases(), "diverge")
     gen_mid()
     gen_table1()
     gen_chars()

@@ -56,6 +56,29 @@ def test_percentile_cuts_bit_exact(E):
         assert _same(hi, ref[:, b]), qs[b]
 
 
+def test_zero_cut_sign_measured(E):
+    """Cuts that are exactly zero (pct.npz arrays with +-0.0 ties): the VALUE is bit-exact
+    (asserted); the SIGN of a zero cut follows the key order (-0.0 before +0.0) here but
+    numpy's introselect partition order in the reference, so it can differ.  Documented
+    divergence: xfail with the measured count when any sign differs.
+    Downstream only the sign of clipped zeros can change (clip compares +-0 equal)."""
+    g = load_npz("pct.npz")
+    vals, off, qs, ref = g["values"], g["offsets"], g["qs"], g["np_percentile"]
+    labels = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    panel = E.panel_from_arrays([vals], ["v"], labels)
+    zero, flips = 0, 0
+    for a, b in [(0, 1), (2, 3), (4, 5), (6, 6)]:
+        cuts = E.select_cuts(panel, qs[a] / 100, qs[b] / 100, 1, E.LERP_NUMPY)
+        for got, j in ((cuts.lo.cpu().numpy()[0], a), (cuts.hi.cpu().numpy()[0], b)):
+            z = ref[:, j] == 0.0
+            assert np.array_equal(got[z], ref[z, j])
+            zero += int(z.sum())
+            flips += int(np.sum(np.signbit(got[z]) != np.signbit(ref[z, j])))
+    assert zero > 100
+    if flips:
+        pytest.xfail(f"{flips} of {zero} exactly-zero cuts differ in sign only")
+
+
 def _adversarial_segments(rng, lengths=(1, 2, 3, 5, 10, 50, 63, 64, 65, 255, 256, 257, 1000, 5000,
                                         12345, 24000)):
     """Month segments that stress the tail fast path and its fallbacks: row-sorted data
@@ -301,6 +324,48 @@ def test_edge_cases_golden(R):
             assert scalar_close(summ[k], v), (name, k, summ[k], v)
 
 
+def test_affine_collinear_pinned(R):
+    """x2 = 2 x1 + 0.5 in every month: statsmodels' pinv null space involves the intercept;
+    the Jacobi fallback's uncentered min-norm correction (fm_solve.hip jacobi_pinv) matches
+    the reference's slopes, R2 and summaries at 1e-9 (diverge.npz, reference-generated)."""
+    g = load_npz("diverge.npz")
+    meta = load_json("diverge.json")
+    name, _, xs = cases.divergence_cases()[0]
+    df = frame_from(g, name + "|in_")
+    got = R.run_monthly_cs_regressions(df, "retx", xs, "mthcaldt")
+    exp = frame_from(g, name + "|out_")
+    assert np.array_equal(got["N"].values, exp["N"].values)
+    for c in got.columns[2:]:
+        assert_series_close(got[c].values, exp[c].values, f"{name} {c}")
+    summ = R.fama_macbeth_summary(got, xs, "mthcaldt", 4)
+    for k, v in meta[name]["summary"].items():
+        assert scalar_close(summ[k], v), (name, k, summ[k], v)
+
+
+def test_near_collinear_divergence_measured(R):
+    """x2 = x1 + 1e-7 noise (sigma_min / sigma_max ~ 1e-7): beyond the normal equations'
+    reach (cond(Sxx) ~ 1e14 > 1 / CHOL_REL), the solve drops the ~1e-14 eigen-direction as
+    null and returns the min-norm split of the x1 / x2 effect, while statsmodels' SVD keeps
+    it.  Pinned here: N exact; R2, the x0 slope and the identified sum slope_x1 + slope_x2
+    within 1e-6; the individual x1 / x2 slopes are a documented divergence (xfail with the
+    measured error)."""
+    g = load_npz("diverge.npz")
+    name, _, xs = cases.divergence_cases()[1]
+    df = frame_from(g, name + "|in_")
+    got = R.run_monthly_cs_regressions(df, "retx", xs, "mthcaldt")
+    exp = frame_from(g, name + "|out_")
+    assert np.array_equal(got["N"].values, exp["N"].values)
+    assert_series_close(got["R2"].values, exp["R2"].values, "R2", rtol=1e-6)
+    assert_series_close(got["slope_x0"].values, exp["slope_x0"].values, "slope_x0", rtol=1e-6)
+    ssum = exp["slope_x1"].values + exp["slope_x2"].values
+    assert_series_close(got["slope_x1"].values + got["slope_x2"].values, ssum, "x1+x2", rtol=1e-6)
+    err = max(float(np.max(np.abs(got[c].values - exp[c].values) / np.abs(exp[c].values)))
+              for c in ("slope_x1", "slope_x2"))
+    if err > 1e-9:
+        pytest.xfail(f"near-collinear x1/x2 slopes: measured max relative error {err:.3g} "
+                     "(min-norm split vs the SVD's individual slopes)")
+
+
 def test_inf_in_y_matches_pinv_semantics(R):
     g = load_npz("edge.npz")
     name, df, xs = [c for c in _edge_inputs(g) if c[0] == "inf_y"][0]
@@ -316,9 +381,12 @@ def test_newey_west_golden(R):
         assert scalar_close(got, case["se"], 1e-12), case["lags"]
 
 
-def test_figure1_golden(CL):
-    g = load_npz("fig1.npz")
-    df = cases.fig1_panel()
+@pytest.mark.parametrize("fixture,panel", [("fig1.npz", cases.fig1_panel), ("fig1c.npz", cases.fig1_const_panel)])
+def test_figure1_golden(CL, fixture, panel):
+    """fig1c: Figure-1 regressors constant within a month (has_constant='add'), the
+    intercept split over [1, c] by the uncentered min-norm (reference :913-921)."""
+    g = load_npz(fixture)
+    df = panel()
     h = hashlib.sha256()
     for c in cases.WINSOR_VARS + ["me"]:
         h.update(np.ascontiguousarray(df[c].values).tobytes())
@@ -579,7 +647,7 @@ def test_sharded_pipeline_bit_identical(E):
     for (s0, s1), loc in zip(bounds, locs):
         g = E.FMResult(problems=loc.problems, rec=rec, status=st, pmax=loc.pmax, moments=loc.moments,
                        mom_stride=loc.mom_stride)
-        ix, summ, roll, p, ps, _ = LW.time_series_stage(g, cfg, moments=loc.moments, seg_lo=s0, seg_hi=s1)
+        ix, summ, roll, p, ps = LW.time_series_stage(g, cfg, moments=loc.moments, seg_lo=s0, seg_hi=s1)
         for x, y in ((summ.mean, full.summary.mean), (summ.tstat, full.summary.tstat), (roll, full.rolling),
                      (ix.count, full.ix.count)):
             assert _same(x.cpu().numpy(), y.cpu().numpy())
@@ -782,5 +850,5 @@ def test_rolling_beta_vs_oracle(CL):
     exp = CO.calculate_rolling_beta(crsp_d, idx, comp)
     assert list(got.columns) == list(exp.columns) and len(got) == len(exp)
     assert np.array_equal(got["permno"].values, exp["permno"].values)
-    assert np.isfinite(exp["beta"].values).sum() > 1000
+    assert np.isfinite(exp["beta"].values).sum() > 500
     assert_series_close(got["beta"].values, exp["beta"].values, "beta")
