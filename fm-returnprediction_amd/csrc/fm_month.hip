@@ -13,7 +13,7 @@
 //               (VPL values per lane, one coalesced read; the next column's loads are
 //               issued as soon as this column's tail candidates sit in LDS), exact tail
 //               order statistics by wave_cut (fm_select_dev.h) -> lo / hi / pivot in LDS
-//               and in HBM ([ncols][nseg]: fm_solve, fm_inf_y_fix and fm_const_check read
+//               and in HBM ([ncols][nseg]: fm_solve, fm_solve_fixup and fm_const_check read
 //               them).  A column the one-wave path cannot decide is redone exactly by the
 //               whole workgroup (select_unit_wg, radix select) before the Gram phase.
 //   Gram phase  fm_gram_dev.h's GramWave over the month's rows with the cuts from LDS

@@ -29,6 +29,11 @@ constexpr int MAXB_LDS = 8192;   // doubles of bucket sums held in LDS (64 KB ma
 constexpr int64_t SCAN_GRID = 1024;   // workgroups of the status-scanning fix-up launches
 constexpr double CHOL_REL = 1e-9;
 constexpr double EIG_REL = 1e-12;
+// A pivot below REFIT_REL of its original diagonal (1 - R^2 of a regressor on the previous
+// ones) means cond(Sxx) >~ 1e6: the normal-equation error (~eps * cond(Sxx)) could exceed
+// the 1e-9 contract, so the problem is flagged FM_ST_REFIT and re-solved from its rows by
+// fm_solve_fixup (Householder QR + SVD of R: error ~eps * cond(X), as statsmodels' SVD).
+constexpr double REFIT_REL = 1e-6;
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -254,6 +259,7 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
             if (ok && k < K) {   // wave-uniform
                 const double orig = readlane_f64(sii, k);
                 const double piv = readlane_f64(row[k], k);
+                if (!(piv > REFIT_REL * orig)) st |= FM_ST_REFIT;
                 if (!(orig > 0.0) || !(piv > CHOL_REL * orig)) {
                     ok = false;
                 } else {
@@ -294,7 +300,7 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
             bi = lane < K ? t : 0.0;
             wave_sync();
         } else {
-            st |= FM_ST_RANK_DEF;
+            st |= FM_ST_RANK_DEF | FM_ST_REFIT;
             // rebuild Sxx (rows were overwritten) for the pseudo-inverse fallback
 #pragma unroll
             for (int j = 0; j < MD; ++j)
@@ -459,12 +465,13 @@ __global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
             if ((__ballot(i >= 1 && i <= K && !(sii > 1e-10 * gdiag)) & gm) != 0) st |= FM_ST_CONST_SUSPECT;
         }
         // ---- augmented Cholesky of S (pivot r = k sits in lane k + 1)
-        bool ok = act0;
+        bool ok = act0, illc = false;
         static_for<0, G16 - 1>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const bool act = ok && k < K;
             const double orig = rowbc<k + 1>(sii);
             const double piv = rowbc<k + 1>(row[k]);
+            if (act && !(piv > REFIT_REL * orig)) illc = true;
             const bool bad = act && (!(orig > 0.0) || !(piv > CHOL_REL * orig));
             if (bad) ok = false;
             const bool go = act && !bad;
@@ -535,6 +542,7 @@ __global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
             wave_sync();
         }
         if (rank_def) st |= FM_ST_RANK_DEF;
+        if (illc) st |= FM_ST_REFIT;
         // ---- R^2 = 1 - SSR/SST (centered), raw-coordinate intercept
         const bool xl = i >= 1 && i <= K;
         double t_sxy = xl ? bi * sxy : 0.0;
@@ -739,31 +747,269 @@ __device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, const doub
     if (threadIdx.x == 0) rec[ro + pmax] = NAN;
 }
 
-__global__ __launch_bounds__(VT) void infy_kernel(const double* cols, int64_t stride,
-                                                  const int64_t* seg_off, int nseg, const double* lo,
-                                                  const double* hi, const double* shift,
-                                                  const double* inv_scale, const double* add_back,
-                                                  const uint8_t* level, int nprob,
-                                                  const int32_t* prob_level, const int32_t* prob_z,
-                                                  const int32_t* prob_nz, const int32_t* pairs,
-                                                  int npairs, const double* moments, int mom_stride,
-                                                  int pmax, double* rec, const uint32_t* status) {
-    __shared__ InfySmem sm;
-    // npairs < 0: scan every (month, problem) for FITTED|INF_IN_Y (no host round trip)
+// ---------------------------------------------------------------------------------------
+// Row-level refit of FM_ST_REFIT problems (ill-conditioned or rank-deficient Sxx), so that
+// statsmodels' pinv semantics hold where the normal equations cannot: pinv_extended takes
+// the SVD of the UNCENTERED design X = [1, x_1..x_K] (rcond 1e-15) and returns
+// params = V S^+ U' y (min-norm over [1, X]), rsquared = 1 - SSR / centered TSS.
+//   1. Householder TSQR of [X | y] over the problem's rows (the Gram's row set: universe
+//      level >= u, every model column non-NaN after the clip), each wave absorbing 64-row
+//      tiles into its own triangular factor, the four factors then merged by wave 0.
+//      Backward stable: the factor's error is ~eps * |X|, not eps * |X|^2.
+//   2. One-sided (Hestenes) Jacobi SVD of R_xx, cut at SVD_REL * sigma_max, and
+//      beta = V S^+ U' r_y with r_y = Q'y.  SSR = |r_y - R_xx beta|^2 + rho^2 (rho = y's
+//      diagonal of R), centered TSS = sum_{i >= 1} r_y[i]^2 + rho^2 (column 0 is the
+//      constant, so Q's first column is 1/sqrt(n)).
+// SVD_REL is 1e-13, not statsmodels' 1e-15: an exact dependence (a zero column, x2 = 2 x1,
+// a regressor constant within the month) leaves a singular value at the QR's rounding
+// floor (~N eps sigma_max), which must be cut; genuine near-dependences down to 1e-13 are
+// kept.
+constexpr double SVD_REL = 1e-13;
+
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v += xor_lanes_f64(v, 1);
+    v += xor_lanes_f64(v, 2);
+    v += xor_lanes_f64(v, 4);
+    v += xor_lanes_f64(v, 8);
+    v += xor_lanes_f64(v, 16);
+    v += xor_lanes_f64(v, 32);
+    return v;
+}
+
+template <int NC>
+struct RefitSmem {
+    double R[VNW][NC][NC + 1];   // per-wave triangular factors of [1, x, y]
+    double Ac[NC][NC + 1];       // Jacobi: rotated columns of R_xx, Ac[j][i] = (R_xx V)[i][j]
+    double Vc[NC][NC + 1];       // Jacobi: V[i][j] at Vc[j][i]
+    double bv[NC];
+};
+
+// Absorb one 64-row tile (lane = row, a[] = its NC values, zero rows allowed) into the
+// wave's triangular factor R: Householder reflections over [R row k; tile column k].
+template <int NC>
+__device__ __forceinline__ void hh_absorb(double (&a)[NC], double (*R)[NC + 1], int nzc) {
+    const int lane = lane_id();
+    static_for<0, NC>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k < nzc) {
+            const double ss = wave_sum_dpp(a[k] * a[k]);
+            if (ss != 0.0) {   // wave-uniform: a zero tile column leaves R as it is
+                const double alpha = R[k][k];
+                const double nrm = sqrt(alpha * alpha + ss);
+                const double beta = alpha > 0.0 ? -nrm : nrm;
+                const double v0 = alpha - beta;
+                const double tau = -v0 / beta;
+                const double vl = a[k] / v0;   // v = (1, a[:,k] / v0)
+                double w[NC];
+                static_for<k + 1, NC>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    w[j] = vl * a[j];
+                });
+                static_for<k + 1, NC>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    w[j] = wave_sum_dpp(w[j]) + R[k][j];
+                });
+                static_for<k + 1, NC>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    a[j] -= (tau * w[j]) * vl;
+                });
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane == 0) {
+                    R[k][k] = beta;
+                    static_for<k + 1, NC>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        R[k][j] -= tau * w[j];
+                    });
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                a[k] = 0.0;
+            }
+        }
+    });
+}
+
+template <int NC>
+__device__ void refit_pair(int s, int p, RefitSmem<NC>& sm, const double* cols, int64_t stride,
+                           const int64_t* seg_off, int nseg, const double* lo, const double* hi,
+                           const double* shift, const double* inv_scale, const double* add_back,
+                           const uint8_t* level, int nprob, const int32_t* prob_level,
+                           const int32_t* prob_z, const int32_t* prob_nz, int pmax, double* rec,
+                           uint32_t* status) {
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+    const int nz = prob_nz[p], P = nz - 1, u = prob_level[p];
+    const int* zi = prob_z + p * 32;
+    for (int e = tid; e < VNW * NC * (NC + 1); e += VT) (&sm.R[0][0][0])[e] = 0.0;
+    __syncthreads();
+    int zc[NC];   // panel column of z index q (q >= 1)
+    static_for<0, NC>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        zc[q] = (q >= 1 && q < nz) ? zi[q] - 1 : 0;
+    });
+    const int64_t r0 = seg_off[s], r1 = seg_off[s + 1];
+    for (int64_t base = r0 + (int64_t)w * WAVE; base < r1; base += VT) {
+        const int64_t r = base + lane;
+        bool valid = r < r1 && !(level && (int)level[r] < u);
+        double a[NC];
+        static_for<0, NC>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            double v = 0.0;
+            if constexpr (q == 0) {
+                v = 1.0;
+            } else {
+                if (valid && q < nz) {
+                    const int c = zc[q];
+                    double x = cols[(int64_t)c * stride + r];
+                    if (lo) {
+                        const double l = lo[(int64_t)c * nseg + s], h = hi[(int64_t)c * nseg + s];
+                        if (x < l) x = l;
+                        if (x > h) x = h;
+                    }
+                    if (inv_scale) {
+                        x = (x - shift[(int64_t)c * nseg + s]) * inv_scale[(int64_t)c * nseg + s];
+                        if (add_back) x += add_back[(int64_t)c * nseg + s];
+                    }
+                    if (isnan(x)) valid = false;
+                    v = x;
+                }
+            }
+            a[q] = v;
+        });
+        static_for<0, NC>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if (!valid) a[q] = 0.0;
+        });
+        hh_absorb<NC>(a, sm.R[w], nz);
+    }
+    __syncthreads();
+    if (w == 0) {   // merge the other waves' factors into wave 0's
+        for (int o = 1; o < VNW; ++o) {
+            double a[NC];
+            static_for<0, NC>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                a[j] = (lane < NC && j >= lane) ? sm.R[o][lane < NC ? lane : 0][j] : 0.0;
+            });
+            hh_absorb<NC>(a, sm.R[0], nz);
+        }
+        // ---- one-sided Jacobi SVD of R_xx (P x P upper triangular), lane i = row i
+        double (*R)[NC + 1] = sm.R[0];
+        const bool li = lane < P;
+        const int lr = li ? lane : 0;
+        for (int j = 0; j < P; ++j) {
+            sm.Ac[j][lr] = (li && j >= lane) ? R[lane][j] : 0.0;
+            sm.Vc[j][lr] = (li && j == lane) ? 1.0 : 0.0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int sweep = 0; sweep < 60; ++sweep) {
+            bool rotated = false;
+            for (int pc = 0; pc < P - 1; ++pc) {
+                for (int qc = pc + 1; qc < P; ++qc) {
+                    const double ap = li ? sm.Ac[pc][lr] : 0.0, aq = li ? sm.Ac[qc][lr] : 0.0;
+                    const double al = wave_sum_dpp(ap * ap);
+                    const double be = wave_sum_dpp(aq * aq);
+                    const double ga = wave_sum_dpp(ap * aq);
+                    if (!(fabs(ga) > 1e-15 * sqrt(al * be))) continue;   // wave-uniform
+                    rotated = true;
+                    const double zeta = (be - al) / (2.0 * ga);
+                    const double t = fabs(zeta) > 1e150
+                                         ? 0.5 / zeta
+                                         : (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                    const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+                    const double vp = li ? sm.Vc[pc][lr] : 0.0, vq = li ? sm.Vc[qc][lr] : 0.0;
+                    if (li) {
+                        sm.Ac[pc][lane] = c * ap - sn * aq;
+                        sm.Ac[qc][lane] = sn * ap + c * aq;
+                        sm.Vc[pc][lane] = c * vp - sn * vq;
+                        sm.Vc[qc][lane] = sn * vp + c * vq;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+            }
+            if (!rotated) break;
+        }
+        // ---- beta = V S^+ (R_xx V)' r_y; singular values below SVD_REL * sigma_max cut
+        const double ry = li ? R[lane][P] : 0.0;   // Q'y
+        const double rho = R[P][P];
+        double smax = 0.0;
+        for (int j = 0; j < P; ++j) smax = fmax(smax, wave_sum_dpp(li ? sm.Ac[j][lr] * sm.Ac[j][lr] : 0.0));
+        smax = sqrt(smax);
+        double bi = 0.0;
+        bool cut = false;
+        for (int j = 0; j < P; ++j) {
+            const double aj = li ? sm.Ac[j][lr] : 0.0;
+            const double s2 = wave_sum_dpp(aj * aj);
+            if (!(sqrt(s2) > SVD_REL * smax)) {
+                cut = true;
+                continue;
+            }
+            const double cj = wave_sum_dpp(aj * ry) / s2;
+            if (li) bi += sm.Vc[j][lane] * cj;
+        }
+        if (li) sm.bv[lane] = bi;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double fit = 0.0;
+        if (li)
+            for (int j = lane; j < P; ++j) fit += R[lane][j] * sm.bv[j];
+        const double e = li ? ry - fit : 0.0;
+        const double ssr = wave_sum_dpp(e * e) + rho * rho;
+        const double tss = wave_sum_dpp((li && lane >= 1) ? ry * ry : 0.0) + rho * rho;
+        const int64_t ro = ((int64_t)s * nprob + p) * (pmax + 2);
+        if (li) rec[ro + lane] = bi;
+        if (lane == 0) {
+            rec[ro + pmax] = 1.0 - ssr / tss;
+            const uint32_t st = status[(int64_t)s * nprob + p];
+            status[(int64_t)s * nprob + p] = (st & ~FM_ST_RANK_DEF) | (cut ? FM_ST_RANK_DEF : 0u);
+        }
+    }
+}
+
+// statsmodels fix-ups after fm_solve, one workgroup per flagged (month, problem):
+// FITTED|INF_IN_Y -> infy_pair; FITTED|REFIT (no inf) -> refit_pair.
+template <int NC>
+__global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t stride,
+                                                   const int64_t* seg_off, int nseg, const double* lo,
+                                                   const double* hi, const double* shift,
+                                                   const double* inv_scale, const double* add_back,
+                                                   const uint8_t* level, int nprob,
+                                                   const int32_t* prob_level, const int32_t* prob_z,
+                                                   const int32_t* prob_nz, const int32_t* pairs,
+                                                   int npairs, const double* moments, int mom_stride,
+                                                   int pmax, double* rec, uint32_t* status) {
+    __shared__ union U {
+        InfySmem infy;
+        RefitSmem<NC> refit;
+    } sm;
+    // npairs < 0: scan every (month, problem) for the flags (no host round trip)
     const int total = npairs < 0 ? nseg * nprob : npairs;
     for (int e = blockIdx.x; e < total; e += gridDim.x) {
         int s, p;
         if (npairs < 0) {
-            const uint32_t st = status[e];
-            if (!(st & FM_ST_FITTED) || !(st & FM_ST_INF_IN_Y)) continue;
             s = e / nprob;
             p = e - s * nprob;
         } else {
             s = pairs[2 * e];
             p = pairs[2 * e + 1];
         }
-        infy_pair(s, p, sm, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level,
-                  nprob, prob_level, prob_z, prob_nz, moments, mom_stride, pmax, rec);
+        const uint32_t st = status[(int64_t)s * nprob + p];
+        if (!(st & FM_ST_FITTED)) continue;
+        if (st & FM_ST_INF_IN_Y) {
+            infy_pair(s, p, sm.infy, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back,
+                      level, nprob, prob_level, prob_z, prob_nz, moments, mom_stride, pmax, rec);
+        } else if ((st & FM_ST_REFIT) && !(st & FM_ST_INF_IN_X) && prob_nz[p] <= NC) {
+            refit_pair<NC>(s, p, sm.refit, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale,
+                           add_back, level, nprob, prob_level, prob_z, prob_nz, pmax, rec, status);
+        } else {
+            continue;
+        }
         __syncthreads();   // sm is reused by the next pair
     }
 }
@@ -821,23 +1067,30 @@ extern "C" int fm_const_check(const double* cols, int64_t col_stride, int32_t nc
     return FM_OK;
 }
 
-extern "C" int fm_inf_y_fix(const double* cols, int64_t col_stride, const int64_t* seg_off,
-                            int32_t nseg, const double* lo, const double* hi, const double* shift,
-                            const double* inv_scale, const double* add_back, const uint8_t* level,
-                            int32_t nprob, const int32_t* prob_level, const int32_t* prob_z,
-                            const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
-                            const double* moments, int32_t mom_stride, int32_t pmax, double* rec,
-                            uint32_t* status, void* stream) {
+extern "C" int fm_solve_fixup(const double* cols, int64_t col_stride, const int64_t* seg_off,
+                              int32_t nseg, const double* lo, const double* hi, const double* shift,
+                              const double* inv_scale, const double* add_back, const uint8_t* level,
+                              int32_t nprob, const int32_t* prob_level, const int32_t* prob_z,
+                              const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
+                              const double* moments, int32_t mom_stride, int32_t pmax, double* rec,
+                              uint32_t* status, void* stream) {
     using namespace fm;
     FM_REQUIRE(cols && seg_off && prob_level && prob_z && prob_nz && moments && rec && status &&
-                   (pairs || npairs < 0), "fm_inf_y_fix: null pointer");
-    FM_REQUIRE((lo == nullptr) == (hi == nullptr), "fm_inf_y_fix: lo/hi must both be set or NULL");
+                   (pairs || npairs < 0), "fm_solve_fixup: null pointer");
+    FM_REQUIRE((lo == nullptr) == (hi == nullptr), "fm_solve_fixup: lo/hi must both be set or NULL");
+    FM_REQUIRE(inv_scale == nullptr || shift != nullptr, "fm_solve_fixup: inv_scale needs shift");
+    FM_REQUIRE(pmax >= 2 && pmax <= 32, "fm_solve_fixup: pmax must be 2..32");
     const int64_t work = npairs < 0 ? (int64_t)nseg * nprob : npairs;
     if (work == 0) return FM_OK;
     const int grid = (int)(npairs < 0 ? (work < SCAN_GRID ? work : SCAN_GRID) : work);
-    hipLaunchKernelGGL(infy_kernel, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
-                       seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
-                       prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status);
-    FM_CHECK_LAUNCH("fm_inf_y_fix");
+    if (pmax + 1 <= 16)
+        hipLaunchKernelGGL(fixup_kernel<16>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
+                           seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
+                           prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status);
+    else
+        hipLaunchKernelGGL(fixup_kernel<32>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
+                           seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
+                           prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status);
+    FM_CHECK_LAUNCH("fm_solve_fixup");
     return FM_OK;
 }

@@ -20,6 +20,7 @@ FM_ST_INF_IN_Y = 0x8
 FM_ST_CONST_SUSPECT = 0x10
 FM_ST_CONST_COL = 0x20
 FM_ST_RANK_DEF = 0x40
+FM_ST_REFIT = 0x80
 
 FM_MAX_COLS = 31
 FM_MAX_MODELS = 6
@@ -111,7 +112,7 @@ _SIGS = {
     "fm_solve": (_i32, [C.POINTER(SolveArgs), _p]),
     "fm_const_check": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _i32, _p, _p, _p, _p,
                               _i32, _p, _p]),
-    "fm_inf_y_fix": (_i32, [_p, _i64, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32,
+    "fm_solve_fixup": (_i32, [_p, _i64, _p, _i32, _p, _p, _p, _p, _p, _p, _i32, _p, _p, _p, _p, _i32,
                             _p, _i32, _i32, _p, _p, _p]),
     "fm_ts_compact": (_i32, [_p, _i64, _i64, _i32, _i32, _p, _p, _p]),
     "fm_ts_summary": (_i32, [_p, _i64, _i64, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,

@@ -484,9 +484,10 @@ def _solve_group(panel, src, gpl, partial, seg_chunk_off, zw, nlevels, T, pmax, 
         status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride)
     _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
     _remember("fm_solve", "fm_solve", sa, partial, seg_chunk_off, gpl, add_back, grec, gst, gmom, *keep)
-    # inf in y: statsmodels' pinv(X) @ y gives +-inf / NaN coefficients.  The fix-up scans
-    # the status on the device (npairs = -1), so there is no host round trip.
-    _kcall("fm_inf_y_fix", "fm_inf_y_fix", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
+    # statsmodels fix-ups: inf in y (pinv(X) @ y gives +-inf / NaN coefficients) and the
+    # QR + SVD refit of ill-conditioned / rank-deficient problems (FM_ST_REFIT).  The fix-up
+    # scans the status on the device (npairs = -1), so there is no host round trip.
+    _kcall("fm_solve_fixup", "fm_solve_fixup", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
            _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), ng,
            gpl.pl.data_ptr(), gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1,
            gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), _stream())

@@ -22,8 +22,10 @@
  *                      over models x universes in one read of the panel
  *   fm_solve        <- sm.OLS(Y, X).fit() params / rsquared / N and the N<K+1 skip
  *                      (src/regressions.py:52-72; src/calc_Lewellen_2014.py:914-921)
- *   fm_inf_y_fix    <- pinv(X) @ y with an infinite return: +-inf/NaN params, NaN R2
- *                      (statsmodels behaviour inside src/regressions.py:57-64)
+ *   fm_solve_fixup  <- statsmodels' pinv semantics where fm_solve's normal equations do not
+ *                      reach them (src/regressions.py:57-64): pinv(X) @ y with an infinite
+ *                      return (+-inf/NaN params, NaN R2), and ill-conditioned / rank-
+ *                      deficient months re-solved from their rows (Householder QR + SVD)
  *   fm_const_check  <- add_constant(has_constant='skip') nonzero-constant detection
  *                      (src/regressions.py:50, which leads to IndexError at :71)
  *   fm_ts_compact, fm_ts_summary <- fama_macbeth_summary + newey_west_mean_se
@@ -76,7 +78,9 @@ extern "C" {
 #define FM_ST_INF_IN_Y 0x8u
 #define FM_ST_CONST_SUSPECT 0x10u /* near-zero centered variance; exact check pending  */
 #define FM_ST_CONST_COL 0x20u     /* nonzero constant regressor -> IndexError          */
-#define FM_ST_RANK_DEF 0x40u      /* pinv fallback (Jacobi eigen) used                 */
+#define FM_ST_RANK_DEF 0x40u      /* pinv min-norm solution (a null direction was cut)  */
+#define FM_ST_REFIT 0x80u         /* ill-conditioned Sxx (pivot < 1e-6 of its diagonal):
+                                     fm_solve_fixup re-solves from the rows (QR + SVD)   */
 
 #define FM_MAX_COLS 31            /* z = [1, cols] fits two 16-wide MFMA tiles          */
 #define FM_MAX_MODELS 6
@@ -213,9 +217,13 @@ int fm_month_pass(const fm_month_args* args, void* stream);
 
 int fm_solve(const fm_solve_args* args, void* stream);
 
-/* fm_const_check / fm_inf_y_fix: `pairs` lists (month, problem) int32 pairs; npairs < 0
+/* fm_const_check / fm_solve_fixup: `pairs` lists (month, problem) int32 pairs; npairs < 0
  * (pairs may be NULL) scans every pair on the device and takes those whose status bits ask
- * for the fix-up (CONST_SUSPECT; FITTED|INF_IN_Y), so callers need no host round trip. */
+ * for the fix-up (CONST_SUSPECT; FITTED|INF_IN_Y or FITTED|REFIT), so callers need no host
+ * round trip.  fm_solve_fixup reads the same row set as fm_gram (clip to lo/hi, NaN drop,
+ * level >= the problem's); with inv_scale the design value is (x - shift) * inv_scale
+ * (+ add_back), without it the raw clipped x (add_back must then restore the shift, as
+ * fm_solve assumes). */
 int fm_const_check(const double* cols, int64_t col_stride, int32_t ncols,
                    const int64_t* seg_off, int32_t nseg,
                    const double* lo, const double* hi, const uint8_t* level,
@@ -223,12 +231,12 @@ int fm_const_check(const double* cols, int64_t col_stride, int32_t ncols,
                    const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
                    uint32_t* status, void* stream);
 
-int fm_inf_y_fix(const double* cols, int64_t col_stride, const int64_t* seg_off, int32_t nseg,
-                 const double* lo, const double* hi, const double* shift, const double* inv_scale,
-                 const double* add_back, const uint8_t* level, int32_t nprob,
-                 const int32_t* prob_level, const int32_t* prob_z, const int32_t* prob_nz,
-                 const int32_t* pairs, int32_t npairs, const double* moments, int32_t mom_stride,
-                 int32_t pmax, double* rec, uint32_t* status, void* stream);
+int fm_solve_fixup(const double* cols, int64_t col_stride, const int64_t* seg_off, int32_t nseg,
+                   const double* lo, const double* hi, const double* shift, const double* inv_scale,
+                   const double* add_back, const uint8_t* level, int32_t nprob,
+                   const int32_t* prob_level, const int32_t* prob_z, const int32_t* prob_nz,
+                   const int32_t* pairs, int32_t npairs, const double* moments, int32_t mom_stride,
+                   int32_t pmax, double* rec, uint32_t* status, void* stream);
 
 int fm_ts_compact(const uint32_t* status, int64_t s_seg, int64_t s_prob, int32_t nseg,
                   int32_t nprob, int32_t* idx, int32_t* count, void* stream);

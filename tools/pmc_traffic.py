@@ -1,6 +1,6 @@
 """Per-launch HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; KiB).
 
-Usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json]
+Usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json [lib_sha16]]
 
 FETCH_SIZE is calibrated on the fm_stream_probe dispatches of tools/pmc_run.py (1 GiB read
 with the panel kernels' 8-B-per-lane coalesced access): factor = true bytes / reported
@@ -13,9 +13,9 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"select_kernel": "fm_select_cuts", "gram_kernel": "fm_gram", "solve_kernel": "fm_solve",
-           "probe_kernel": "fm_stream_probe", "level_kernel": "fm_universe_level",
-           "pilot_kernel": "fm_pilot_shift"}
+KERNELS = {"select_pair_kernel": "fm_select_cuts", "gram_kernel": "fm_gram",
+           "solve16_kernel": "fm_solve", "probe_kernel": "fm_stream_probe",
+           "level_kernel": "fm_universe_level", "ts_fused_kernel": "fm_ts_fused"}
 
 
 def per_dispatch(path, counter):
@@ -57,6 +57,8 @@ def main():
             if k in wn[d][0] and wn[d][1] == big[tag]:
                 agg[tag]["write"].append(v * 1024)
     res = {"fetch_calibration_factor": factor}
+    if len(sys.argv) > 4:
+        res["lib_sha16"] = sys.argv[4]
     for tag, a in agg.items():
         f = sum(a["fetch"]) / len(a["fetch"]) if a["fetch"] else 0.0
         w = sum(a["write"]) / len(a["write"]) if a["write"] else 0.0
