@@ -363,10 +363,19 @@ def cpu_baseline(panel, args, LW):
     else:
         O.pipeline_arrays(cols, seg, me, nyse, models, None)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "firm-month rows/s", "cores": 1, "kind": "port",
-            "seconds": dt,
+    out = {"value": n / dt, "unit": "firm-month rows/s", "cores": 1, "kind": "port",
+           "seconds": dt,
             "sample": f"first {S} months x {args.firms} firms of the same panel, full pass "
                       f"(11 problems/month, rolling, forecasts), oracle/fm_oracle.py, 1 BLAS thread"}
+    # the port vs the reference itself, timed side by side in the build container
+    # (tools/ref_vs_port_timing.py -> profiles/ref_vs_port.json; the reference never travels)
+    rp = os.path.join(ROOT, "profiles", "ref_vs_port.json")
+    if os.path.exists(rp):
+        d = json.load(open(rp))
+        out["ref_over_port"] = d["ref_over_port"]
+        out["reference_value_est"] = out["value"] * d["ref_over_port"]
+        out["ref_over_port_sample"] = d["sample"] + f", python {d['interpreter']}, profiles/ref_vs_port.json"
+    return out
 
 
 def check_against_oracle(panel, gres, summ, args, LW):
