@@ -686,6 +686,56 @@ def test_pipeline_c5_month_width(E):
     _pipeline_vs_oracle(E, 12, 20000, 7)
 
 
+def test_pipeline_c5_rank_shard_full_size(E):
+    """C5 at full per-rank size: one of 8 ranks' shards of the 100,000-month x 20,000-firm
+    panel (12,500 months x 20,000 firms = 250M rows, 30 GB of FP64 columns in HBM, seed
+    20150101, months 50,000..62,499 as rank 4 would generate them) through run_pipeline.
+    The 12,500-month series exceeds the fused time-series kernel's LDS staging, so the
+    per-stage kernels run.  Checked: (1) four sampled months' monthly records against the
+    oracle run on exactly those months (host regeneration of the same counter-hash rows);
+    (2) the FM summaries (mean, NW t) and the 120/60 rolling means against the oracle's
+    restatement applied to the device's own monthly records (12,500-long series)."""
+    import torch
+    from fmcore import lewellen as LW, synth
+    T, N, seed, m0 = 12500, 20000, 20150101, 50000
+    panel = E.panel_synthetic(T, N, seed, month0=m0)
+    cfg = LW.PipelineConfig()
+    assert not E.ts_fused_fits(T, 16, cfg.window, cfg.lag, predictive=True)
+    out = LW.run_pipeline(panel, cfg)
+    torch.cuda.synchronize()
+    res = out.res
+    rec = res.rec.cpu().numpy()
+    st = res.status.cpu().numpy()
+    models = {name: ("retx", xs, (0, 1, 2)) for name, xs in LW.table2_models().items()}
+    models["Figure 1"] = ("retx", LW.FIG1_VARS, (0, 2))
+    for t in (0, 1, T // 2, T - 1):
+        a = synth.synth_arrays(1, N, seed, month0=m0 + t)
+        cols = {c: a[c] for c in synth.WINSOR_VARS}
+        ref = O.pipeline_arrays(cols, np.array([0, N], dtype=np.int64), a["me"], a["nyse"].astype(bool),
+                                models, None)
+        for k, p in enumerate(res.problems):
+            r = ref[(out.model_names[p.model], p.level)]
+            assert (st[t, k] & 1) != 0 and list(r["month"]) == [0], (t, k)
+            assert int(rec[t, k, res.pmax + 1]) == int(r["N"][0])
+            b = r["params"][0]
+            a_ = rec[t, k, :p.K + 1]
+            assert np.all(np.abs(a_ - b) <= RTOL * np.maximum(np.abs(b), np.sqrt(np.mean(b ** 2)))), (t, k)
+            assert abs(rec[t, k, res.pmax] - r["R2"][0]) <= RTOL * abs(r["R2"][0])
+    mean = out.summary.mean.cpu().numpy()
+    tstat = out.summary.tstat.cpu().numpy()
+    roll = out.rolling.cpu().numpy()
+    for k, p in enumerate(res.problems):
+        fit = np.nonzero(st[:, k] & 1)[0]
+        assert fit.size == T
+        for j in range(1, p.K + 1):
+            x = rec[fit, k, j]
+            m = x.mean()
+            assert scalar_close(mean[k, j], m, RTOL, 1e-12), (k, j)
+            assert scalar_close(tstat[k, j], m / O.newey_west_mean_se(x, 4), RTOL, 1e-12), (k, j)
+        for j in range(2):   # intercept and first slope (the restatement loops per row)
+            assert_series_close(roll[k, :T, j], O.rolling_mean(rec[fit, k, j], 120, 60), f"roll {k}/{j}")
+
+
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
 def test_pipeline_single_model_configs(E, cfg):
     """C1 (Model 1, K=3) and C2 (Model 2, K=7) alone, 3 universes, no Figure 1."""
