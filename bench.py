@@ -190,7 +190,7 @@ def main():
         kern[tag] = timer.avg_ms(tag)   # events around each eager launch (incl. launch gaps)
     fused = "fm_month_pass" in E.LAST_LAUNCH
     tags = (("fm_month_pass",) if fused else ("fm_select_cuts", "fm_gram")) + \
-        ("fm_select_cuts[nyse]", "fm_solve", "fm_ts_fused", "fm_ts_fused[pred]")
+        ("fm_universe", "fm_solve", "fm_ts_fused", "fm_ts_fused[pred]")
     dev_ms = {t: E.time_launch(t) for t in tags if t in E.LAST_LAUNCH}
     # algorithmic HBM bytes per launch: every panel column once (8 B per
     # value), the universe level byte, and the month tables written (cuts, pivots, Gram

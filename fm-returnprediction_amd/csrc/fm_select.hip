@@ -553,6 +553,78 @@ void launch_select_wave(const SelArgs& a, hipStream_t st) {
         hipLaunchKernelGGL((select_wave_kernel<VPL, false>), dim3((unsigned)select_wave_grid(nunits)), dim3(ST), 0, st, a);
 }
 
+// get_subsets' NYSE breakpoints AND the nested universe levels in one launch (reference
+// src/calc_Lewellen_2014.py:69-105): one 256-thread workgroup per month holds the month's
+// `me` in registers (VPT per thread, one coalesced read, the NYSE flags as a bit mask),
+// finds the pandas groupby.quantile(q_a, q_b) order statistics of the NYSE rows (NaN me
+// skipped) by the adaptive histogram select, lerps them the pandas way, and writes every
+// row's level (me >= me_20) + (me >= me_50) from the same registers (NaN compares False).
+#ifndef FM_AB_UNI_NOSELECT
+#define FM_AB_UNI_NOSELECT 0   // timing builds only (tools/build_variant.sh): skip the order statistics
+#endif
+template <int VPT>
+__global__ __launch_bounds__(ST) void universe_kernel(const double* __restrict__ me,
+                                                      const uint8_t* __restrict__ nyse,
+                                                      const int64_t* __restrict__ seg_off, double qa,
+                                                      double qb, double* __restrict__ cut_a,
+                                                      double* __restrict__ cut_b,
+                                                      uint8_t* __restrict__ level) {
+    static_assert(VPT <= 64, "universe_kernel: NYSE flags are one 64-bit mask per thread");
+    __shared__ SelSmem sm;
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const int64_t r0 = seg_off[s];
+    const int L = (int)(seg_off[s + 1] - r0);
+    const int last = L > 0 ? L - 1 : 0;
+    double xm[VPT];
+    uint64_t nb = 0;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {   // unconditional (clamped) loads, masked after
+        const int idx = tid + v * ST;
+        const int ci = idx < L ? idx : last;
+        const double x = me[r0 + ci];
+        const uint8_t m = nyse[r0 + ci];
+        xm[v] = idx < L ? x : NAN;
+        if (idx < L && m != 0 && !isnan(x)) nb |= 1ull << v;
+    }
+    auto for_each = [&](auto&& f) {
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) f(((nb >> v) & 1ull) ? xm[v] : NAN);
+    };
+    int cnt = 0;
+    uint64_t kmn = SENT, kmx = 0;
+    for_each([&](double x) {
+        if (!isnan(x)) {
+            ++cnt;
+            const uint64_t k = dkey(x);
+            kmn = k < kmn ? k : kmn;
+            kmx = k > kmx ? k : kmx;
+        }
+    });
+    const int n = block_sum<SNW>(cnt, sm.ints);
+    kmn = block_min_u64<SNW>(kmn, sm.u64s);
+    kmx = block_max_u64<SNW>(kmx, sm.u64s + SNW);
+    double a = NAN, b = NAN;
+    if (n > 0) {   // block-uniform
+        int rk[4];
+        double g0, g1;
+        qranks(n, qa, 1, rk[0], rk[1], g0);
+        qranks(n, qb, 1, rk[2], rk[3], g1);
+        uint64_t ko[4] = {kmn, kmn, kmx, kmx};
+        if (!FM_AB_UNI_NOSELECT) hist_select(for_each, 4, rk, kmn, kmx, ko, sm);
+        a = qlerp(kval(ko[0]), kval(ko[1]), g0, 1);
+        b = qlerp(kval(ko[2]), kval(ko[3]), g1, 1);
+    }
+    if (tid == 0) {
+        cut_a[s] = a;
+        cut_b[s] = b;
+    }
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const int idx = tid + v * ST;
+        if (idx < L) level[r0 + idx] = (uint8_t)((xm[v] >= a ? 1 : 0) + (xm[v] >= b ? 1 : 0));
+    }
+}
+
 }  // namespace
 }  // namespace fm
 
@@ -632,5 +704,28 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
     else if (vpt <= 64) launch_select<64>(a, ncols, st, wave);
     else launch_select<96>(a, ncols, st, wave);
     FM_CHECK_LAUNCH("fm_select_cuts");
+    return FM_OK;
+}
+
+extern "C" int fm_universe(const double* me, const uint8_t* nyse, const int64_t* seg_off, int32_t nseg,
+                           int32_t max_seg_len, double q_a, double q_b, double* cut_a, double* cut_b,
+                           uint8_t* level, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(me && nyse && seg_off && cut_a && cut_b && level, "fm_universe: null pointer");
+    FM_REQUIRE(nseg >= 0 && max_seg_len >= 0, "fm_universe: bad sizes");
+    FM_REQUIRE(q_a >= 0.0 && q_a <= 1.0 && q_b >= 0.0 && q_b <= 1.0, "fm_universe: quantiles must be in [0,1]");
+    if (max_seg_len > 64 * ST) {
+        set_error("fm_universe: %d-row months exceed %d (use fm_select_cuts + fm_universe_level)",
+                  max_seg_len, 64 * ST);
+        return FM_ETOOBIG;
+    }
+    if (nseg == 0) return FM_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int vpt = (max_seg_len + ST - 1) / ST;
+    if (vpt <= 8) hipLaunchKernelGGL(universe_kernel<8>, dim3(nseg), dim3(ST), 0, st, me, nyse, seg_off, q_a, q_b, cut_a, cut_b, level);
+    else if (vpt <= 20) hipLaunchKernelGGL(universe_kernel<20>, dim3(nseg), dim3(ST), 0, st, me, nyse, seg_off, q_a, q_b, cut_a, cut_b, level);
+    else if (vpt <= 32) hipLaunchKernelGGL(universe_kernel<32>, dim3(nseg), dim3(ST), 0, st, me, nyse, seg_off, q_a, q_b, cut_a, cut_b, level);
+    else hipLaunchKernelGGL(universe_kernel<64>, dim3(nseg), dim3(ST), 0, st, me, nyse, seg_off, q_a, q_b, cut_a, cut_b, level);
+    FM_CHECK_LAUNCH("fm_universe");
     return FM_OK;
 }

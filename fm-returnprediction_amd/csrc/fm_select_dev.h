@@ -785,11 +785,17 @@ __device__ __forceinline__ void pick_tail(const double* L, int c, int ra, int rb
     }
     wave_sort_f64<R>(v);
     auto at = [&](int e) -> double {
-        double x = v[0];
-#pragma unroll
-        for (int r = 1; r < R; ++r)
-            if ((e >> 6) == r) x = v[r];   // e is wave-uniform
-        return __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(x), e & 63));
+        // lane e & 63 of every register read out (scalar), then a scalar pick of register
+        // e >> 6: selecting the register first becomes a dynamically indexed stack array
+        // (scratch round trips)
+        const int q = e >> 6, l = e & 63;
+        uint64_t x = readlane_u64((uint64_t)__double_as_longlong(v[0]), l);
+        static_for<1, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            const uint64_t t = readlane_u64((uint64_t)__double_as_longlong(v[r]), l);
+            x = q == r ? t : x;
+        });
+        return __longlong_as_double((long long)x);
     };
     va = ra < c ? at(ra) : tau;
     vb = rb < c ? at(rb) : tau;
@@ -809,11 +815,17 @@ __device__ __forceinline__ void pick_tail2(const double* L1, int c1, const doubl
     }
     wave_sort_f64<R>(v);
     auto at = [&](int e) -> double {
-        double x = v[0];
-#pragma unroll
-        for (int r = 1; r < R; ++r)
-            if ((e >> 6) == r) x = v[r];   // e is wave-uniform
-        return __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(x), e & 63));
+        // lane e & 63 of every register read out (scalar), then a scalar pick of register
+        // e >> 6: selecting the register first becomes a dynamically indexed stack array
+        // (scratch round trips)
+        const int q = e >> 6, l = e & 63;
+        uint64_t x = readlane_u64((uint64_t)__double_as_longlong(v[0]), l);
+        static_for<1, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            const uint64_t t = readlane_u64((uint64_t)__double_as_longlong(v[r]), l);
+            x = q == r ? t : x;
+        });
+        return __longlong_as_double((long long)x);
     };
     va = ra < c ? at(ra) : tau;
     vb = rb < c ? at(rb) : tau;

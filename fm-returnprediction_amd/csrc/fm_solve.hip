@@ -34,6 +34,9 @@ constexpr double EIG_REL = 1e-12;
 // the 1e-9 contract, so the problem is flagged FM_ST_REFIT and re-solved from its rows by
 // fm_solve_fixup (Householder QR + SVD of R: error ~eps * cond(X), as statsmodels' SVD).
 constexpr double REFIT_REL = 1e-6;
+#ifndef FM_AB_SOLVE_NOMOM
+#define FM_AB_SOLVE_NOMOM 0   // timing builds only (tools/build_variant.sh): skip the moments store
+#endif
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -129,6 +132,32 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(v), l));
 }
 
+// Sum the month's chunk partials into LDS: BCH loads per thread in flight per chunk (a
+// one-load-per-iteration loop waits out one HBM round trip per element).
+template <int NT>
+__device__ __forceinline__ void sum_partials(const double* partial, int c0, int c1, int n, double* bs) {
+    constexpr int BCH = 8;
+    const int tid = threadIdx.x;
+    for (int e0 = tid; e0 < n; e0 += NT * BCH) {
+        double acc[BCH];
+#pragma unroll
+        for (int k = 0; k < BCH; ++k) acc[k] = 0.0;
+        for (int c = c0; c < c1; ++c) {
+            const double* pc = partial + (int64_t)c * n;
+#pragma unroll
+            for (int k = 0; k < BCH; ++k) {
+                const int e = e0 + k * NT;
+                acc[k] += pc[e < n ? e : n - 1];   // clamped: unconditional loads
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < BCH; ++k) {
+            const int e = e0 + k * NT;
+            if (e < n) bs[e] = acc[k];
+        }
+    }
+}
+
 // Per month: bucket sums -> level-cumulative sums (bucket (pattern, u) becomes the sum over
 // levels >= u, so a problem adds one bucket per pattern that contains its model) -> one
 // wave per problem.  The wave keeps the centered moment matrix S over (x_1..x_K, y) in
@@ -147,11 +176,7 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
     const int zw = a.zw, zz = zw * (zw + 1) / 2;   // packed upper triangle per bucket
     const int nl = a.nlevels, npat = a.npatterns, nb = npat * nl;
     const int c0 = a.seg_chunk_off[s], c1 = a.seg_chunk_off[s + 1];
-    for (int e = tid; e < nb * zz; e += VT) {
-        double acc = 0.0;
-        for (int c = c0; c < c1; ++c) acc += a.partial[(int64_t)c * nb * zz + e];
-        bs[e] = acc;
-    }
+    sum_partials<VT>(a.partial, c0, c1, nb * zz, bs);
     __syncthreads();
     for (int e = tid; e < npat * zz; e += VT) {
         const int pid = e / zz, f = e - pid * zz;
@@ -365,26 +390,27 @@ __device__ __forceinline__ double rowsum(double v) {
 
 constexpr int G16 = 16;   // lanes per problem
 
-__global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
+// 128 threads (two waves, eight problems at a time) at two waves per SIMD: 256 VGPRs (the
+// factorization's register rows and columns fit without spills) and four workgroups per
+// CU, so every month of a 600-month panel is resident at once.
+constexpr int S16T = 128;
+constexpr int S16W = S16T / WAVE;
+__global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     extern __shared__ double bs[];   // [nb][136] packed bucket sums of this month
     // per wave: four transpose tiles, or (afterwards, one problem at a time) the Jacobi
-    // fallback's scratch; the union keeps three workgroups per CU (all months resident)
+    // fallback's scratch (a union)
     constexpr int TT = G16 * (G16 + 1);
     static_assert(sizeof(WaveScratch<16>) <= 4 * TT * sizeof(double), "scratch union");
-    __shared__ double wsc[VNW][4 * TT];
+    __shared__ double wsc[S16W][4 * TT];
     const int s = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1);
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
     constexpr int zw = 16, zz = 136;
     const int nl = a.nlevels, npat = a.npatterns, nb = npat * nl;
     const int c0 = a.seg_chunk_off[s], c1 = a.seg_chunk_off[s + 1];
-    for (int e = tid; e < nb * zz; e += VT) {
-        double acc = 0.0;
-        for (int c = c0; c < c1; ++c) acc += a.partial[(int64_t)c * nb * zz + e];
-        bs[e] = acc;
-    }
+    sum_partials<S16T>(a.partial, c0, c1, nb * zz, bs);
     __syncthreads();
-    for (int e = tid; e < npat * zz; e += VT) {   // level-cumulative buckets
+    for (int e = tid; e < npat * zz; e += S16T) {   // level-cumulative buckets
         const int pid = e / zz, f = e - pid * zz;
         double* b0 = bs + (int64_t)pid * nl * zz + f;
         double run = b0[(nl - 1) * zz];
@@ -397,30 +423,35 @@ __global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
     const int g = lane >> 4, i = lane & 15;
     const int rs = a.pmax + 2;
     double* T = wsc[w] + g * TT;
-    for (int p0 = w * 4; p0 < a.nprob; p0 += VNW * 4) {
+    for (int p0 = w * 4; p0 < a.nprob; p0 += S16W * 4) {
         const int p = p0 + g;
         const bool live = p < a.nprob;
         const int pp = live ? p : p0;
         const int m = a.prob_model[pp], u = a.prob_level[pp], nz = a.prob_nz[pp];
         const int K = nz - 2, K1 = K + 1;
         const int zi = i < nz ? a.prob_z[pp * 32 + i] : 0;   // z index of this lane's row
-        // ---- row i of the problem Gram: one level-cumulative bucket per pattern with m
-        int off[G16];
-        static_for<0, G16>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            const int zj = rowbc_i<j>(zi);
-            const int r = zi < zj ? zi : zj, c = zi < zj ? zj : zi;
-            off[j] = r * zw - (r * (r - 1)) / 2 + (c - r);
-        });
+        // ---- row i of the problem Gram: one level-cumulative bucket per pattern with m.
+        // A lambda, so the rare rank-deficient path re-reads G from LDS instead of keeping it
+        // (and the offsets) live through the factorization: 48 VGPRs, no spills at 3 waves/SIMD
+        auto gram_row = [&](double (&G)[G16]) {
+            int off[G16];
+            static_for<0, G16>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                const int zj = rowbc_i<j>(zi);
+                const int r = zi < zj ? zi : zj, c = zi < zj ? zj : zi;
+                off[j] = r * zw - (r * (r - 1)) / 2 + (c - r);
+            });
+#pragma unroll
+            for (int j = 0; j < G16; ++j) G[j] = 0.0;
+            for (int q = 0; q < npat; ++q) {
+                if (!((a.pattern_models[q] >> m) & 1u)) continue;   // per problem
+                const double* bq = bs + (q * nl + u) * zz;
+#pragma unroll
+                for (int j = 0; j < G16; ++j) G[j] += bq[off[j]];
+            }
+        };
         double G[G16];
-#pragma unroll
-        for (int j = 0; j < G16; ++j) G[j] = 0.0;
-        for (int q = 0; q < npat; ++q) {
-            if (!((a.pattern_models[q] >> m) & 1u)) continue;   // per problem
-            const double* bq = bs + (q * nl + u) * zz;
-#pragma unroll
-            for (int j = 0; j < G16; ++j) G[j] += bq[off[j]];
-        }
+        gram_row(G);
         const double n = rowbc<0>(G[0]);
         // centered moments: lane i (1 <= i <= K1) holds S row r = i - 1, S[r][c] in row[c]
         const bool srow = i >= 1 && i <= K1;
@@ -451,7 +482,7 @@ __global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
             if (i == 0) a.status[(int64_t)s * a.nprob + pp] = FM_ST_SKIPPED;
         }
         const bool act0 = live && !skip;
-        if (act0 && a.moments) {
+        if (act0 && a.moments && !FM_AB_SOLVE_NOMOM) {
             double* mo = a.moments + ((int64_t)s * a.nprob + pp) * a.mom_stride;
             if (i == 0) mo[0] = n;
             if (srow) {
@@ -516,10 +547,13 @@ __global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
         double bi = (ok && i >= 1 && i <= K) ? t : 0.0;   // slope of x_{i-1}
         // ---- rank-deficient problems of this wave: Jacobi pseudo-inverse, one at a time
         const uint64_t rd = __ballot(rank_def && i == 0);
+        double G2[G16];
+        if (rd) gram_row(G2);   // wave-uniform
         for (uint64_t q = rd; q; q &= q - 1) {
             const int gq = __builtin_ctzll(q) >> 4;   // wave-uniform
             WaveScratch<16>& J = *reinterpret_cast<WaveScratch<16>*>(wsc[w]);
             const int Kq = __shfl(K, gq * 16, WAVE);
+            const double (&G)[G16] = G2;
             // rebuild Sxx (rows were overwritten) from G, the shuffles with every lane active
             {
                 double g0c[G16 - 1];
@@ -576,27 +610,11 @@ __global__ __launch_bounds__(VT, 3) void solve16_kernel(fm_solve_args a) {
 
 // Exact nonzero-constant test for problems flagged CONST_SUSPECT (statsmodels
 // add_constant(has_constant='skip'): np.ptp(x)==0 & all(x != 0), src/regressions.py:50).
-__global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t stride, int ncols,
-                                                   const int64_t* seg_off, int nseg,
-                                                   const double* lo, const double* hi,
-                                                   const uint8_t* level, int nprob,
-                                                   const int32_t* prob_level, const int32_t* prob_z,
-                                                   const int32_t* prob_nz, const int32_t* pairs,
-                                                   int npairs, uint32_t* status) {
-    __shared__ uint64_t red[VNW];
-    // npairs < 0: scan every (month, problem) and take those the solve flagged, so the
-    // check needs no host round trip; else the listed pairs.
-    const int total = npairs < 0 ? nseg * nprob : npairs;
-    for (int e = blockIdx.x; e < total; e += gridDim.x) {
-    int s, p;
-    if (npairs < 0) {
-        s = e / nprob;
-        p = e - s * nprob;
-        if (!(status[e] & FM_ST_CONST_SUSPECT)) continue;
-    } else {
-        s = pairs[2 * e];
-        p = pairs[2 * e + 1];
-    }
+__device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, const double* cols, int64_t stride,
+                                           const int64_t* seg_off, int nseg, const double* lo,
+                                           const double* hi, const uint8_t* level, int nprob,
+                                           const int32_t* prob_level, const int32_t* prob_z,
+                                           const int32_t* prob_nz, uint32_t* status) {
     const int nz = prob_nz[p], K = nz - 2, u = prob_level[p];
     const int* zi = prob_z + p * 32;
     const int64_t r0 = seg_off[s], r1 = seg_off[s + 1];
@@ -632,6 +650,31 @@ __global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t s
         if (kmin != SENT && kmin == kmax && nzr == 0) any_const = true;
     }
     if (threadIdx.x == 0 && any_const) status[(int64_t)s * nprob + p] |= FM_ST_CONST_COL;
+}
+
+__global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t stride, int ncols,
+                                                   const int64_t* seg_off, int nseg,
+                                                   const double* lo, const double* hi,
+                                                   const uint8_t* level, int nprob,
+                                                   const int32_t* prob_level, const int32_t* prob_z,
+                                                   const int32_t* prob_nz, const int32_t* pairs,
+                                                   int npairs, uint32_t* status) {
+    __shared__ uint64_t red[VNW];
+    // npairs < 0: scan every (month, problem) and take those the solve flagged, so the
+    // check needs no host round trip; else the listed pairs.
+    const int total = npairs < 0 ? nseg * nprob : npairs;
+    for (int e = blockIdx.x; e < total; e += gridDim.x) {
+        int s, p;
+        if (npairs < 0) {
+            s = e / nprob;
+            p = e - s * nprob;
+            if (!(status[e] & FM_ST_CONST_SUSPECT)) continue;
+        } else {
+            s = pairs[2 * e];
+            p = pairs[2 * e + 1];
+        }
+        const_pair(s, p, red, cols, stride, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
+                   prob_nz, status);
     }
 }
 
@@ -898,10 +941,11 @@ __device__ void refit_pair(int s, int p, RefitSmem<NC>& sm, const double* cols, 
         double (*R)[NC + 1] = sm.R[0];
         const bool li = lane < P;
         const int lr = li ? lane : 0;
-        for (int j = 0; j < P; ++j) {
-            sm.Ac[j][lr] = (li && j >= lane) ? R[lane][j] : 0.0;
-            sm.Vc[j][lr] = (li && j == lane) ? 1.0 : 0.0;
-        }
+        if (li)
+            for (int j = 0; j < P; ++j) {
+                sm.Ac[j][lane] = j >= lane ? R[lane][j] : 0.0;
+                sm.Vc[j][lane] = j == lane ? 1.0 : 0.0;
+            }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -973,7 +1017,8 @@ __device__ void refit_pair(int s, int p, RefitSmem<NC>& sm, const double* cols, 
 }
 
 // statsmodels fix-ups after fm_solve, one workgroup per flagged (month, problem):
-// FITTED|INF_IN_Y -> infy_pair; FITTED|REFIT (no inf) -> refit_pair.
+// CONST_SUSPECT (with check_const) -> const_pair; FITTED|INF_IN_Y -> infy_pair;
+// FITTED|REFIT (no inf) -> refit_pair.
 template <int NC>
 __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t stride,
                                                    const int64_t* seg_off, int nseg, const double* lo,
@@ -983,10 +1028,12 @@ __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t s
                                                    const int32_t* prob_level, const int32_t* prob_z,
                                                    const int32_t* prob_nz, const int32_t* pairs,
                                                    int npairs, const double* moments, int mom_stride,
-                                                   int pmax, double* rec, uint32_t* status) {
+                                                   int pmax, double* rec, uint32_t* status,
+                                                   int check_const) {
     __shared__ union U {
         InfySmem infy;
         RefitSmem<NC> refit;
+        uint64_t red[VNW];
     } sm;
     // npairs < 0: scan every (month, problem) for the flags (no host round trip)
     const int total = npairs < 0 ? nseg * nprob : npairs;
@@ -1000,6 +1047,12 @@ __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t s
             p = pairs[2 * e + 1];
         }
         const uint32_t st = status[(int64_t)s * nprob + p];
+        const bool cst = check_const && (st & FM_ST_CONST_SUSPECT);
+        if (cst) {
+            const_pair(s, p, sm.red, cols, stride, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
+                       prob_nz, status);
+            __syncthreads();
+        }
         if (!(st & FM_ST_FITTED)) continue;
         if (st & FM_ST_INF_IN_Y) {
             infy_pair(s, p, sm.infy, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back,
@@ -1040,7 +1093,7 @@ extern "C" int fm_solve(const fm_solve_args* args, void* stream) {
         attr_set = true;
     }
     if (a.zw == 16)
-        hipLaunchKernelGGL(solve16_kernel, dim3(a.nseg), dim3(VT), dyn, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(solve16_kernel, dim3(a.nseg), dim3(S16T), dyn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(solve_kernel<32>, dim3(a.nseg), dim3(VT), dyn, (hipStream_t)stream, a);
     FM_CHECK_LAUNCH("fm_solve");
@@ -1073,7 +1126,7 @@ extern "C" int fm_solve_fixup(const double* cols, int64_t col_stride, const int6
                               int32_t nprob, const int32_t* prob_level, const int32_t* prob_z,
                               const int32_t* prob_nz, const int32_t* pairs, int32_t npairs,
                               const double* moments, int32_t mom_stride, int32_t pmax, double* rec,
-                              uint32_t* status, void* stream) {
+                              uint32_t* status, int32_t check_const, void* stream) {
     using namespace fm;
     FM_REQUIRE(cols && seg_off && prob_level && prob_z && prob_nz && moments && rec && status &&
                    (pairs || npairs < 0), "fm_solve_fixup: null pointer");
@@ -1086,11 +1139,11 @@ extern "C" int fm_solve_fixup(const double* cols, int64_t col_stride, const int6
     if (pmax + 1 <= 16)
         hipLaunchKernelGGL(fixup_kernel<16>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
                            seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
-                           prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status);
+                           prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status, check_const);
     else
         hipLaunchKernelGGL(fixup_kernel<32>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
                            seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
-                           prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status);
+                           prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status, check_const);
     FM_CHECK_LAUNCH("fm_solve_fixup");
     return FM_OK;
 }

@@ -317,9 +317,21 @@ __host__ __device__ __forceinline__ size_t ts_ix_bytes(int T) { return ((size_t)
 __device__ __forceinline__ int ts_compact_lds(const fm_ts_args& a, int p, int* ixs, int* wtot) {
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
     int base = 0;
-    for (int s0 = 0; s0 < a.nseg; s0 += FT) {
+    constexpr int PF = 8;   // status words per thread loaded before the first scan (in flight together)
+    for (int sb = 0; sb < a.nseg; sb += PF * FT) {
+    uint32_t sw[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {   // clamped, unconditional loads
+        const int s = sb + k * FT + tid;
+        const int sc = s < a.nseg ? s : a.nseg - 1;
+        sw[k] = a.status[(int64_t)sc * a.s_seg + (int64_t)p * a.s_prob];
+    }
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        const int s0 = sb + k * FT;
+        if (s0 >= a.nseg) break;   // block-uniform
         const int s = s0 + tid;
-        const bool f = s < a.nseg && (a.status[(int64_t)s * a.s_seg + (int64_t)p * a.s_prob] & FM_ST_FITTED);
+        const bool f = s < a.nseg && (sw[k] & FM_ST_FITTED);
         const uint64_t bm = __ballot(f);
         if (lane == 0) wtot[w] = (int)__popcll(bm);
         __syncthreads();
@@ -334,6 +346,7 @@ __device__ __forceinline__ int ts_compact_lds(const fm_ts_args& a, int p, int* i
         base += tot;
         __syncthreads();
     }
+    }
     return base;
 }
 
@@ -341,7 +354,19 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
                               int* wtot, double* dred) {
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
     const double* rk = a.rec + (int64_t)p * a.r_prob + k;
-    for (int i = tid; i < cnt; i += FT) xs[i] = rk[(int64_t)ixs[i] * a.r_seg];   // all in flight
+    for (int i0 = 0; i0 < cnt; i0 += 8 * FT) {   // 8 gathers per thread in flight together
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * FT + tid;
+            v[k] = rk[(int64_t)ixs[i < cnt ? i : cnt - 1] * a.r_seg];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * FT + tid;
+            if (i < cnt) xs[i] = v[k];
+        }
+    }
     __syncthreads();
     // dropna in place, month order kept (each pass reads its span before any write lands)
     int n = 0;

@@ -273,6 +273,28 @@ def universe_level(panel: DevicePanel, cut_a, cut_b):
     return level
 
 
+def universe(panel: DevicePanel, q_a=0.2, q_b=0.5):
+    """get_subsets on the device (reference src/calc_Lewellen_2014.py:69-105): the NYSE
+    me_20 / me_50 breakpoints and the nested universe level byte of every row, one launch
+    (fm_universe); months longer than its register budget take fm_select_cuts (row mask)
+    + fm_universe_level.  Returns (cut_a [T], cut_b [T], level [rows] uint8)."""
+    if panel.max_seg_len > UNIVERSE_MAX_ROWS:
+        a, b = nyse_breakpoints(panel, q_a, q_b)
+        return a, b, universe_level(panel, a, b)
+    dev = panel.cols.device
+    a = torch.empty(panel.nseg, dtype=torch.float64, device=dev)
+    b = torch.empty_like(a)
+    level = torch.empty(panel.nrows, dtype=torch.uint8, device=dev)
+    args = (panel.me.data_ptr(), panel.nyse.data_ptr(), panel.seg_off.data_ptr(), panel.nseg,
+            max(panel.max_seg_len, 0), float(q_a), float(q_b), a.data_ptr(), b.data_ptr(), level.data_ptr())
+    _kcall("fm_universe", "fm_universe", *args, _stream())
+    _remember("fm_universe", "fm_universe", None, (panel.me, panel.nyse, panel.seg_off, a, b, level), args)
+    return a, b, level
+
+
+UNIVERSE_MAX_ROWS = 64 * 256   # fm_universe's register budget (one workgroup per month)
+
+
 def pilot_shift(panel: DevicePanel, cols=None):
     src = panel.cols if cols is None else cols
     sh = torch.empty((src.shape[0], panel.nseg), dtype=torch.float64, device=src.device)
@@ -484,18 +506,15 @@ def _solve_group(panel, src, gpl, partial, seg_chunk_off, zw, nlevels, T, pmax, 
         status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride)
     _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
     _remember("fm_solve", "fm_solve", sa, partial, seg_chunk_off, gpl, add_back, grec, gst, gmom, *keep)
-    # statsmodels fix-ups: inf in y (pinv(X) @ y gives +-inf / NaN coefficients) and the
-    # QR + SVD refit of ill-conditioned / rank-deficient problems (FM_ST_REFIT).  The fix-up
-    # scans the status on the device (npairs = -1), so there is no host round trip.
+    # statsmodels fix-ups in one launch: the exact nonzero-constant test where the solve saw a
+    # near-zero variance (CONST_SUSPECT), inf in y (pinv(X) @ y gives +-inf / NaN
+    # coefficients) and the QR + SVD refit of ill-conditioned / rank-deficient problems
+    # (FM_ST_REFIT).  It scans the status on the device (npairs = -1): no host round trip.
     _kcall("fm_solve_fixup", "fm_solve_fixup", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
            _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), ng,
            gpl.pl.data_ptr(), gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1,
-           gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), _stream())
-    # exact nonzero-constant test where the Gram flagged a near-zero variance
-    if const_check:
-        _kcall("fm_const_check", "fm_const_check", src.data_ptr(), src.stride(0), src.shape[0],
-               panel.seg_off.data_ptr(), T, _ptr(lo), _ptr(hi), _ptr(level), ng, gpl.pl.data_ptr(),
-               gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1, gst.data_ptr(), _stream())
+           gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), int(bool(const_check)),
+           _stream())
     return grec, gst, gmom
 
 

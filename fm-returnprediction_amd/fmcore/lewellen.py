@@ -108,16 +108,6 @@ def build_models(panel: E.DevicePanel, model_cols: Dict[str, List[str]], y="retx
     return models, names
 
 
-_SIDE = {}
-
-
-def _side_stream(device):
-    s = _SIDE.get(str(device))
-    if s is None:
-        s = _SIDE[str(device)] = torch.cuda.Stream(device=device)
-    return s
-
-
 def _standardize_params(panel: E.DevicePanel, cuts: E.Cuts, yi: int):
     """A9 (build-defined): the Gram sees z = (clip(x) - mean_t) / sd_t for every predictor
     column (shift = mean, inv_scale = 1/sd, nothing added back: the regressors ARE the
@@ -137,34 +127,24 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
     cuts = None
     shift = None
     inv_scale = None
-    # The NYSE breakpoints (600 latency-bound units) run on a side stream, concurrently with
-    # the bandwidth-bound winsorize cuts; the Gram waits for both (a fork/join that HIP graph
-    # capture records as two parallel branches).
     level, bp = None, None
     nlevels = 1
-    main = torch.cuda.current_stream()
-    side = None
     models, names = build_models(panel, model_cols, y=y, fig1=cfg.fig1, universes=cfg.universes)
     if cfg.fused_month and cfg.winsorize and not cfg.standardize and \
             E.month_pass_fits(panel, models, 3 if cfg.universes else 1):
         # fused path: NYSE breakpoints + universe levels, then ONE launch per pass doing the
         # winsorize cuts and the batched Gram month by month (fm_month_pass)
         if cfg.universes:
-            a, b = E.nyse_breakpoints(panel)
-            level = E.universe_level(panel, a, b)
+            a, b, level = E.universe(panel)
             nlevels = 3
             bp = (a, b)
         res, cuts = E.month_pass(panel, models, level=level, nlevels=nlevels, q_lo=cfg.lower_percentile / 100,
                                  q_hi=cfg.upper_percentile / 100, min_count=5, moments=cfg.forecasts)
         return res, names, cuts, level, bp
     if cfg.universes:
-        side = _side_stream(main.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            a, b = E.nyse_breakpoints(panel)
-            level = E.universe_level(panel, a, b)
-        for t in (a, b, level):
-            t.record_stream(main)
+        # one launch, on the pass's own stream: a side-stream fork / join inside the captured
+        # graph cost more in cross-queue synchronization than the overlap saved
+        a, b, level = E.universe(panel)
         nlevels = 3
         bp = (a, b)
     add_back = None
@@ -180,8 +160,6 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
         if not cfg.winsorize:
             cuts = E.Cuts(torch.full_like(cuts.lo, float("nan")), torch.full_like(cuts.hi, float("nan")),
                           cuts.nvalid, cuts.mean, cuts.sd, cuts.center)
-    if side is not None:
-        main.wait_stream(side)
     res = E.fm_pass(panel, models, level=level, nlevels=nlevels, cuts=cuts, shift=shift,
                     inv_scale=inv_scale, add_back=add_back if cfg.standardize else shift,
                     moments=cfg.forecasts)

@@ -50,8 +50,7 @@ def _nyse_cuts(df):
     me = _api.as_f64(df["me"])
     nyse = (df["primaryexch"] == "N").to_numpy().astype(np.uint8)
     panel = _E.panel_from_arrays([me], ["me"], df["mthcaldt"].values, me=me, nyse=nyse)
-    a, b = _E.nyse_breakpoints(panel)
-    level = _E.universe_level(panel, a, b)
+    a, b, level = _E.universe(panel)
     return panel, a.cpu().numpy(), b.cpu().numpy(), level.cpu().numpy()
 
 

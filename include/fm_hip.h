@@ -16,6 +16,8 @@
  *   fm_clip         <- subdf[var].clip(lower, upper) (src/calc_Lewellen_2014.py:524)
  *   fm_standardize  <- per-month z-score (north-star extension; no reference line)
  *   fm_universe_level <- me >= me_20 / me >= me_50 masks (src/calc_Lewellen_2014.py:95-96)
+ *   fm_universe     <- get_subsets in one launch: the NYSE groupby.quantile([.2,.5]) of me
+ *                      (src/calc_Lewellen_2014.py:74-82) and the nested masks (:95-105)
  *   fm_pilot_shift  <- (numerics only) per-month pivot used to center the Gram
  *   fm_gram         <- dropna (src/regressions.py:39) + X'X, X'y, y'y inside sm.OLS
  *                      (src/regressions.py:57; src/calc_Lewellen_2014.py:917-919), batched
@@ -186,6 +188,15 @@ int fm_standardize(const double* src, double* dst, int64_t col_stride, int32_t n
 int fm_universe_level(const double* me, const int64_t* seg_off, int32_t nseg, int64_t nrows,
                       const double* cut_a, const double* cut_b, uint8_t* level, void* stream);
 
+/* fm_universe: per month the pandas-lerp q_a / q_b quantiles of `me` over rows with
+ * nyse != 0 (NaN me skipped; no such row -> NaN cuts) into cut_a / cut_b [nseg], and every
+ * row's level (me >= cut_a) + (me >= cut_b) (NaN compares False).  Months of at most
+ * 64 * 256 rows; longer ones return FM_ETOOBIG (fm_select_cuts with a row mask +
+ * fm_universe_level do any length). */
+int fm_universe(const double* me, const uint8_t* nyse, const int64_t* seg_off, int32_t nseg,
+                int32_t max_seg_len, double q_a, double q_b, double* cut_a, double* cut_b,
+                uint8_t* level, void* stream);
+
 int fm_pilot_shift(const double* cols, int64_t col_stride, int32_t ncols,
                    const int64_t* seg_off, int32_t nseg, double* shift, void* stream);
 
@@ -220,7 +231,8 @@ int fm_solve(const fm_solve_args* args, void* stream);
 /* fm_const_check / fm_solve_fixup: `pairs` lists (month, problem) int32 pairs; npairs < 0
  * (pairs may be NULL) scans every pair on the device and takes those whose status bits ask
  * for the fix-up (CONST_SUSPECT; FITTED|INF_IN_Y or FITTED|REFIT), so callers need no host
- * round trip.  fm_solve_fixup reads the same row set as fm_gram (clip to lo/hi, NaN drop,
+ * round trip.  With check_const != 0, fm_solve_fixup also runs fm_const_check's test on
+ * the CONST_SUSPECT pairs (one launch for every fix-up).  It reads the same row set as fm_gram (clip to lo/hi, NaN drop,
  * level >= the problem's); with inv_scale the design value is (x - shift) * inv_scale
  * (+ add_back), without it the raw clipped x (add_back must then restore the shift, as
  * fm_solve assumes). */
@@ -236,7 +248,7 @@ int fm_solve_fixup(const double* cols, int64_t col_stride, const int64_t* seg_of
                    const double* add_back, const uint8_t* level, int32_t nprob,
                    const int32_t* prob_level, const int32_t* prob_z, const int32_t* prob_nz,
                    const int32_t* pairs, int32_t npairs, const double* moments, int32_t mom_stride,
-                   int32_t pmax, double* rec, uint32_t* status, void* stream);
+                   int32_t pmax, double* rec, uint32_t* status, int32_t check_const, void* stream);
 
 int fm_ts_compact(const uint32_t* status, int64_t s_seg, int64_t s_prob, int32_t nseg,
                   int32_t nprob, int32_t* idx, int32_t* count, void* stream);

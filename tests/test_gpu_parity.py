@@ -198,6 +198,45 @@ def test_masked_middle_quantiles_hist_select(E):
         assert _same([b[t]], [O.pandas_quantile(x[m], 0.5)]), t
 
 
+def test_universe_kernel_vs_oracle(E):
+    """fm_universe (NYSE me_20 / me_50 + the nested level byte, one launch) against the
+    pandas lerp restatement and the reference's masks (me >= cut, NaN False): months of
+    1 .. 16,384 rows (the register budget's edge), lognormal / clustered / tied keys, NaN me
+    on NYSE and non-NYSE rows, a month without NYSE rows and one whose NYSE me are all NaN."""
+    rng = np.random.default_rng(55)
+    segs, masks = [], []
+    for n in (1, 2, 7, 300, 5000, 16384):
+        for kind in ("lognormal", "cluster", "ties"):
+            x = np.exp(rng.normal(5, 2, n)) if kind == "lognormal" else _hard_segment(rng, n, kind)
+            x[rng.random(n) < 0.05] = np.nan
+            segs.append(x)
+            masks.append(rng.random(n) < 0.4)
+    segs.append(np.exp(rng.normal(5, 2, 900)))
+    masks.append(np.zeros(900, dtype=bool))                       # no NYSE row
+    x = np.exp(rng.normal(5, 2, 900))
+    m = rng.random(900) < 0.4
+    x[m] = np.nan
+    segs.append(x)
+    masks.append(m)                                               # every NYSE me NaN
+    vals = np.concatenate(segs)
+    mask = np.concatenate(masks).astype(np.uint8)
+    labels = np.repeat(np.arange(len(segs)), [len(x) for x in segs])
+    panel = E.panel_from_arrays([vals], ["me"], labels, me=vals, nyse=mask)
+    assert panel.max_seg_len <= E.UNIVERSE_MAX_ROWS
+    a, b, level = E.universe(panel)
+    assert "fm_universe" in E.LAST_LAUNCH
+    a, b, level = a.cpu().numpy(), b.cpu().numpy(), level.cpu().numpy()
+    off = panel.seg_off_h
+    for t, (x, m) in enumerate(zip(segs, masks)):
+        v = x[m & ~np.isnan(x)]
+        ea = O.pandas_quantile(v, 0.2) if v.size else np.nan
+        eb = O.pandas_quantile(v, 0.5) if v.size else np.nan
+        assert _same([a[t]], [ea]) and _same([b[t]], [eb]), t
+        with np.errstate(invalid="ignore"):
+            exp = (x >= ea).astype(np.uint8) + (x >= eb).astype(np.uint8)
+        assert np.array_equal(level[off[t]:off[t + 1]], exp), t
+
+
 def test_pandas_quantile_bit_exact(E):
     g = load_npz("pct.npz")
     vals, off, ref = g["values"], g["offsets"], g["pd_quantile"]

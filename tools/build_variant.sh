@@ -1,0 +1,20 @@
+#!/bin/bash
+# Timing variants of libfm_hip.so for tools/kbench.py A/B runs (never shipped):
+#   tools/build_variant.sh <name> "<extra hipcc flags>" [source.hip ...]
+# Reuses the in-tree objects and recompiles only the listed sources with the extra flags
+# into build_variants/<name>/libfm_hip.so.
+set -e
+name=$1; flags=$2; shift 2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+CS=$ROOT/fm-returnprediction_amd/csrc
+VD=$ROOT/build_variants/$name
+mkdir -p "$VD/obj"
+cp -p "$CS"/build/*.o "$VD/obj/"
+for src in "$@"; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I"$ROOT/include" \
+    -Wall -Wno-unused-function $flags -c "$CS/$src" -o "$VD/obj/${src%.hip}.o" &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$VD"/obj/*.o -o "$VD/libfm_hip.so"
+rm -rf "$VD/obj"
+echo "$VD/libfm_hip.so"

@@ -15,7 +15,7 @@ from collections import defaultdict
 
 KERNELS = {"select_pair_kernel": "fm_select_cuts", "gram_kernel": "fm_gram",
            "solve16_kernel": "fm_solve", "probe_kernel": "fm_stream_probe",
-           "level_kernel": "fm_universe_level", "ts_fused_kernel": "fm_ts_fused"}
+           "universe_kernel": "fm_universe", "ts_fused_kernel": "fm_ts_fused"}
 
 
 def per_dispatch(path, counter):
