@@ -563,7 +563,7 @@ void launch_select_wave(const SelArgs& a, hipStream_t st) {
 #define FM_AB_UNI_NOSELECT 0   // timing builds only (tools/build_variant.sh): skip the order statistics
 #endif
 template <int VPT>
-__global__ __launch_bounds__(ST) void universe_kernel(const double* __restrict__ me,
+__global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const double* __restrict__ me,
                                                       const uint8_t* __restrict__ nyse,
                                                       const int64_t* __restrict__ seg_off, double qa,
                                                       double qb, double* __restrict__ cut_a,
