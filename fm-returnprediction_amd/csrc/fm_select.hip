@@ -312,6 +312,25 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
         }
         return L;
     };
+    // finite min / max of this wave's half of unit u, re-read from memory: only the rare
+    // pivot fallback (no finite cut midpoint) needs it, and by then xv holds the next unit
+    auto finite_range = [&](int64_t uu, double& m1, double& m2) {
+        const int s = (int)(uu % a.nseg), c = (int)(uu / a.nseg);
+        const double* base = a.cols + (int64_t)c * a.col_stride + a.seg_off[s];
+        const int Lu = (int)(a.seg_off[s + 1] - a.seg_off[s]);
+        m1 = NAN;
+        m2 = NAN;
+        for (int r = h * WAVE + lane; r < Lu; r += 2 * WAVE) {
+            const double x = base[r];
+            m1 = hw_min(m1, isfinite(x) ? x : NAN);
+            m2 = hw_max(m2, isfinite(x) ? x : NAN);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            m1 = hw_min(m1, xor_lanes_f64(m1, o));
+            m2 = hw_max(m2, xor_lanes_f64(m2, o));
+        }
+    };
     int L = load(k);
     while (true) {
         const int64_t u = unit_of(a, k);
@@ -394,6 +413,7 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
             ok = sm.okv[0] != 0 && sm.okv[1] != 0;   // block-uniform
         }
         double lo = NAN, hi = NAN;
+        bool prefetched = false;
         if (ok) {
             // ---- 3. compaction of this wave's half into its own lists
             int clo = 0, chi = 0;
@@ -417,6 +437,9 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
                 sm.ni[h][1] = clo;
                 sm.ni[h][2] = chi;
             }
+            // xv is dead from here on: the next unit's loads fly during the candidate sorts
+            if (more) Ln = load(kn);
+            prefetched = true;
             __syncthreads();
             // ---- 4. one tail per wave over both halves' candidates
             const int t = h;
@@ -443,17 +466,8 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
         } else if (h == 0) {
             double cen = 0.5 * (lo + hi);
             if (!isfinite(cen)) {
-                double m1 = NAN, m2 = NAN;
-#pragma unroll
-                for (int v = 0; v < VPH; ++v) {
-                    m1 = hw_min(m1, isfinite(xv[v]) ? xv[v] : NAN);
-                    m2 = hw_max(m2, isfinite(xv[v]) ? xv[v] : NAN);
-                }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    m1 = hw_min(m1, xor_lanes_f64(m1, o));
-                    m2 = hw_max(m2, xor_lanes_f64(m2, o));
-                }
+                double m1, m2;
+                finite_range(u, m1, m2);
                 if (lane == 0) sm.res[0] = m1, sm.res[1] = m2;
             }
             if (lane == 0) {
@@ -464,20 +478,11 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
             }
         } else if (!isfinite(0.5 * (lo + hi))) {
             // wave 1's half of the finite range for the pivot fallback
-            double m1 = NAN, m2 = NAN;
-#pragma unroll
-            for (int v = 0; v < VPH; ++v) {
-                m1 = hw_min(m1, isfinite(xv[v]) ? xv[v] : NAN);
-                m2 = hw_max(m2, isfinite(xv[v]) ? xv[v] : NAN);
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                m1 = hw_min(m1, xor_lanes_f64(m1, o));
-                m2 = hw_max(m2, xor_lanes_f64(m2, o));
-            }
+            double m1, m2;
+            finite_range(u, m1, m2);
             if (lane == 0) sm.tv[0] = m1, sm.tv[1] = m2;
         }
-        if (more) Ln = load(kn);   // xv is dead: the next unit's loads fly across the barrier
+        if (more && !prefetched) Ln = load(kn);   // the next unit's loads fly across the barrier
         __syncthreads();
         if ((ok || !apply) && a.center && !isfinite(0.5 * (lo + hi)) && threadIdx.x == 0) {
             // pivot fallback: the midpoint of the finite range (both halves), else 0
