@@ -1035,35 +1035,57 @@ __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t s
         RefitSmem<NC> refit;
         uint64_t red[VNW];
     } sm;
-    // npairs < 0: scan every (month, problem) for the flags (no host round trip)
+    // npairs < 0: scan every (month, problem) for the flags (no host round trip).  Each
+    // workgroup reads VT status words at once and lists the flagged pairs in LDS (a
+    // pair-by-pair scan would wait out one memory round trip per pair), then fixes them.
+    __shared__ int flagged[VT];
+    __shared__ int nflag;
     const int total = npairs < 0 ? nseg * nprob : npairs;
-    for (int e = blockIdx.x; e < total; e += gridDim.x) {
-        int s, p;
-        if (npairs < 0) {
-            s = e / nprob;
-            p = e - s * nprob;
-        } else {
-            s = pairs[2 * e];
-            p = pairs[2 * e + 1];
+    const int tid = threadIdx.x;
+    for (int base = blockIdx.x * VT; base < total; base += gridDim.x * VT) {
+        if (tid == 0) nflag = 0;
+        __syncthreads();
+        {
+            const int e = base + tid;
+            if (e < total) {
+                int s, p;
+                if (npairs < 0) {
+                    s = e / nprob;
+                    p = e - s * nprob;
+                } else {
+                    s = pairs[2 * e];
+                    p = pairs[2 * e + 1];
+                }
+                const uint32_t st = status[(int64_t)s * nprob + p];
+                const bool want = (check_const && (st & FM_ST_CONST_SUSPECT)) ||
+                                  ((st & FM_ST_FITTED) && (st & (FM_ST_INF_IN_Y | FM_ST_REFIT)));
+                if (want) flagged[atomicAdd(&nflag, 1)] = s * nprob + p;
+            }
         }
-        const uint32_t st = status[(int64_t)s * nprob + p];
-        const bool cst = check_const && (st & FM_ST_CONST_SUSPECT);
-        if (cst) {
-            const_pair(s, p, sm.red, cols, stride, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
-                       prob_nz, status);
-            __syncthreads();
+        __syncthreads();
+        const int nf = nflag;
+        for (int f = 0; f < nf; ++f) {
+            const int sp = flagged[f];
+            const int s = sp / nprob, p = sp - s * nprob;
+            const uint32_t st = status[(int64_t)s * nprob + p];
+            if (check_const && (st & FM_ST_CONST_SUSPECT)) {
+                const_pair(s, p, sm.red, cols, stride, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
+                           prob_nz, status);
+                __syncthreads();
+            }
+            if (!(st & FM_ST_FITTED)) continue;
+            if (st & FM_ST_INF_IN_Y) {
+                infy_pair(s, p, sm.infy, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back,
+                          level, nprob, prob_level, prob_z, prob_nz, moments, mom_stride, pmax, rec);
+            } else if ((st & FM_ST_REFIT) && !(st & FM_ST_INF_IN_X) && prob_nz[p] <= NC) {
+                refit_pair<NC>(s, p, sm.refit, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale,
+                               add_back, level, nprob, prob_level, prob_z, prob_nz, pmax, rec, status);
+            } else {
+                continue;
+            }
+            __syncthreads();   // sm is reused by the next pair
         }
-        if (!(st & FM_ST_FITTED)) continue;
-        if (st & FM_ST_INF_IN_Y) {
-            infy_pair(s, p, sm.infy, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back,
-                      level, nprob, prob_level, prob_z, prob_nz, moments, mom_stride, pmax, rec);
-        } else if ((st & FM_ST_REFIT) && !(st & FM_ST_INF_IN_X) && prob_nz[p] <= NC) {
-            refit_pair<NC>(s, p, sm.refit, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale,
-                           add_back, level, nprob, prob_level, prob_z, prob_nz, pmax, rec, status);
-        } else {
-            continue;
-        }
-        __syncthreads();   // sm is reused by the next pair
+        __syncthreads();   // the list is rebuilt for the next range
     }
 }
 
@@ -1135,7 +1157,8 @@ extern "C" int fm_solve_fixup(const double* cols, int64_t col_stride, const int6
     FM_REQUIRE(pmax >= 2 && pmax <= 32, "fm_solve_fixup: pmax must be 2..32");
     const int64_t work = npairs < 0 ? (int64_t)nseg * nprob : npairs;
     if (work == 0) return FM_OK;
-    const int grid = (int)(npairs < 0 ? (work < SCAN_GRID ? work : SCAN_GRID) : work);
+    const int64_t ranges = (work + VT - 1) / VT;   // VT pairs per workgroup pass
+    const int grid = (int)(ranges < SCAN_GRID ? ranges : SCAN_GRID);
     if (pmax + 1 <= 16)
         hipLaunchKernelGGL(fixup_kernel<16>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
                            seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
