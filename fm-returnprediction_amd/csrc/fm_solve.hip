@@ -395,6 +395,7 @@ constexpr int G16 = 16;   // lanes per problem
 // CU, so every month of a 600-month panel is resident at once.
 constexpr int S16T = 128;
 constexpr int S16W = S16T / WAVE;
+constexpr int S16_MAXP = 32;   // problems per group held in LDS tables
 __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     extern __shared__ double bs[];   // [nb][136] packed bucket sums of this month
     // per wave: four transpose tiles, or (afterwards, one problem at a time) the Jacobi
@@ -407,6 +408,25 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
     constexpr int zw = 16, zz = 136;
     const int nl = a.nlevels, npat = a.npatterns, nb = npat * nl;
+    // The small per-problem tables and this month's add-back values go to LDS first, all
+    // loads issued together with the partials' (read in place, each would be a dependent
+    // memory round trip inside the problem loop)
+    __shared__ int t_model[S16_MAXP], t_level[S16_MAXP], t_nz[S16_MAXP], t_flags[S16_MAXP];
+    __shared__ uint8_t t_z[S16_MAXP][32];
+    __shared__ uint32_t t_pat[64];
+    __shared__ double t_ab[32];
+    for (int e = tid; e < a.nprob * 32; e += S16T) t_z[e >> 5][e & 31] = (uint8_t)a.prob_z[e];
+    if (tid < a.nprob) {
+        t_model[tid] = a.prob_model[tid];
+        t_level[tid] = a.prob_level[tid];
+        t_nz[tid] = a.prob_nz[tid];
+        t_flags[tid] = a.prob_flags[tid];
+    }
+    if (tid < npat) t_pat[tid] = a.pattern_models[tid];
+    if (a.add_back && tid >= 64 && tid < 96) {
+        const int c = tid - 64;   // panel columns past ncols are never indexed
+        t_ab[c] = c < a.ab_ncols ? a.add_back[(int64_t)c * a.nseg + s] : 0.0;
+    }
     const int c0 = a.seg_chunk_off[s], c1 = a.seg_chunk_off[s + 1];
     sum_partials<S16T>(a.partial, c0, c1, nb * zz, bs);
     __syncthreads();
@@ -427,9 +447,9 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         const int p = p0 + g;
         const bool live = p < a.nprob;
         const int pp = live ? p : p0;
-        const int m = a.prob_model[pp], u = a.prob_level[pp], nz = a.prob_nz[pp];
+        const int m = t_model[pp], u = t_level[pp], nz = t_nz[pp];
         const int K = nz - 2, K1 = K + 1;
-        const int zi = i < nz ? a.prob_z[pp * 32 + i] : 0;   // z index of this lane's row
+        const int zi = i < nz ? t_z[pp][i] : 0;   // z index of this lane's row
         // ---- row i of the problem Gram: one level-cumulative bucket per pattern with m.
         // A lambda, so the rare rank-deficient path re-reads G from LDS instead of keeping it
         // (and the offsets) live through the factorization: 48 VGPRs, no spills at 3 waves/SIMD
@@ -444,7 +464,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
 #pragma unroll
             for (int j = 0; j < G16; ++j) G[j] = 0.0;
             for (int q = 0; q < npat; ++q) {
-                if (!((a.pattern_models[q] >> m) & 1u)) continue;   // per problem
+                if (!((t_pat[q] >> m) & 1u)) continue;   // per problem
                 const double* bq = bs + (q * nl + u) * zz;
 #pragma unroll
                 for (int j = 0; j < G16; ++j) G[j] += bq[off[j]];
@@ -492,7 +512,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                     if (c < K1) mo[1 + K1 + (i - 1) * K1 + c] = row[c];
             }
         }
-        if (act0 && (a.prob_flags[pp] & 1) != 0) {
+        if (act0 && (t_flags[pp] & 1) != 0) {
             if ((__ballot(i >= 1 && i <= K && !(sii > 1e-10 * gdiag)) & gm) != 0) st |= FM_ST_CONST_SUSPECT;
         }
         // ---- augmented Cholesky of S (pivot r = k sits in lane k + 1)
@@ -567,7 +587,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                     J.sxy[i - 1] = sxy;
                 }
                 if (g == gq && i >= 1 && i <= Kq + 1)   // raw means of x_0..x_{K-1}, y
-                    J.mu[i - 1] = mu + (a.add_back ? a.add_back[(int64_t)(zi - 1) * a.nseg + s] : 0.0);
+                    J.mu[i - 1] = mu + (a.add_back ? t_ab[zi - 1] : 0.0);
             }
             wave_sync();
             if (lane == 0) jacobi_pinv<16>(J.A, J.V, Kq, J.sxy, J.mu, J.b);
@@ -581,18 +601,18 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         const bool xl = i >= 1 && i <= K;
         double t_sxy = xl ? bi * sxy : 0.0;
         double t_mu = xl ? bi * mu : 0.0;
-        double t_ab = 0.0;
-        if (a.add_back && xl && act0) t_ab = bi * a.add_back[(int64_t)(zi - 1) * a.nseg + s];
+        double t_abx = 0.0;
+        if (a.add_back && xl && act0) t_abx = bi * t_ab[zi - 1];
         t_sxy = rowsum(t_sxy);
         t_mu = rowsum(t_mu);
-        t_ab = rowsum(t_ab);
+        t_abx = rowsum(t_abx);
         const double syy = __shfl(sii, g * 16 + (K1 < 16 ? K1 : 15), WAVE);   // S[K][K]
         const double muy = __shfl(mu, g * 16 + (K1 < 16 ? K1 : 15), WAVE);
         const double r2 = 1.0 - (syy - t_sxy) / syy;
         double icpt = muy - t_mu;
         if (a.add_back && act0) {
-            const int zy = a.prob_z[pp * 32 + K + 1];
-            icpt += a.add_back[(int64_t)(zy - 1) * a.nseg + s] - t_ab;
+            const int zy = t_z[pp][K + 1];
+            icpt += t_ab[zy - 1] - t_abx;
         }
         if (act0) {
             for (int k = i; k < rs; k += G16) {
@@ -1104,6 +1124,9 @@ extern "C" int fm_solve(const fm_solve_args* args, void* stream) {
                "fm_solve: %d buckets of a %d-wide Gram exceed the LDS budget", a.npatterns * a.nlevels, a.zw);
     FM_REQUIRE(a.pmax >= 2 && a.pmax <= 32, "fm_solve: pmax must be 2..32");
     FM_REQUIRE(a.moments == nullptr || a.mom_stride > 0, "fm_solve: bad mom_stride");
+    FM_REQUIRE(a.add_back == nullptr || (a.ab_ncols >= 1 && a.ab_ncols <= FM_MAX_COLS),
+               "fm_solve: add_back needs ab_ncols in 1..%d", FM_MAX_COLS);
+    FM_REQUIRE(a.zw == 32 || a.nprob <= S16_MAXP, "fm_solve: at most %d problems per group", S16_MAXP);
     if (a.nseg == 0 || a.nprob == 0) return FM_OK;
     const size_t dyn = (size_t)a.npatterns * a.nlevels * (a.zw * (a.zw + 1) / 2) * sizeof(double);
     static bool attr_set = false;

@@ -82,7 +82,7 @@ class SolveArgs(C.Structure):
         ("nprob", _i32), ("prob_model", _p), ("prob_level", _p), ("prob_z", _p),
         ("prob_nz", _p), ("prob_flags", _p), ("add_back", _p), ("gram_flags", _p),
         ("nmodels", _i32), ("pmax", _i32), ("rec", _p), ("status", _p),
-        ("moments", _p), ("mom_stride", _i32),
+        ("moments", _p), ("mom_stride", _i32), ("ab_ncols", _i32),
     ]
 
 

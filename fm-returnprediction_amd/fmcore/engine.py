@@ -503,7 +503,7 @@ def _solve_group(panel, src, gpl, partial, seg_chunk_off, zw, nlevels, T, pmax, 
         prob_model=gpl.pm.data_ptr(), prob_level=gpl.pl.data_ptr(), prob_z=gpl.pz.data_ptr(),
         prob_nz=gpl.pnz.data_ptr(), prob_flags=gpl.pf.data_ptr(), add_back=_ptr(add_back),
         gram_flags=None, nmodels=gpl.nmodels, pmax=pmax, rec=grec.data_ptr(),
-        status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride)
+        status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride, ab_ncols=src.shape[0])
     _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
     _remember("fm_solve", "fm_solve", sa, partial, seg_chunk_off, gpl, add_back, grec, gst, gmom, *keep)
     # statsmodels fix-ups in one launch: the exact nonzero-constant test where the solve saw a

@@ -136,6 +136,7 @@ typedef struct fm_solve_args {
     uint32_t* status;             /* [nseg][nprob] FM_ST_* bits */
     double* moments;              /* [nseg][nprob][mom_stride] or NULL: n, means(K+1), centered (K+1)^2 */
     int32_t mom_stride;
+    int32_t ab_ncols;             /* rows of add_back ([ab_ncols][nseg]; the panel's ncols) */
 } fm_solve_args;
 
 const char* fm_version(void);
