@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-chars", action="store_true", help="skip the firm-characteristic stage")
     ap.add_argument("--check", action="store_true", help="verify one step against the oracle")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 per-rank shard measurement")
     return ap.parse_args()
 
 
@@ -250,10 +251,38 @@ def main():
         result["firm_chars"] = firm_chars_stage(args, E)
     if args.check and rank == 0 and world == 1:
         result["check"] = check_against_oracle(panel, gres, summ, args, LW)
+    if rank == 0 and world == 1 and not args.no_c5:
+        del panel
+        torch.cuda.empty_cache()
+        result["c5_rank_shard"] = c5_shard_stage(args, E, LW)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def c5_shard_stage(args, E, LW, reps=3):
+    """C5 (BASELINE configs[4]: 100,000 months x 20,000 firms x 15 chars over 8 GPUs) at one
+    rank's size: 12,500 months x 20,000 firms = 250M rows (30 GB of FP64 columns) generated
+    in HBM as rank 4 would, one full pass (winsorize, universes, 11 problems/month, the
+    12,500-month time series on the per-stage kernels), timed eagerly (events around the
+    pass).  The gather of the other ranks' records is not part of this single-GPU figure."""
+    T, N = 12500, 20000
+    p = E.panel_synthetic(T, N, 20150101, month0=4 * T)
+    cfg = LW.PipelineConfig()
+    LW.run_pipeline(p, cfg)   # warm-up (plans, workspaces)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        LW.run_pipeline(p, cfg)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    rows = T * N
+    return {"rows": rows, "months": T, "firms": N, "ms_per_pass": ms, "rows_per_s": rows / (ms * 1e-3),
+            "whole_pass_frac": rows * (15 * 8 + 8 + 1) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "note": "eager launches; one rank of the 8-GPU C5 split"}
 
 
 def _lib_sha():

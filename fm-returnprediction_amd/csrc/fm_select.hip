@@ -21,6 +21,13 @@
 
 #include "fm_select_dev.h"
 
+#ifndef FM_SELECT_STREAM_VPT
+#define FM_SELECT_STREAM_VPT 24   // values per thread above which fm_select streams the units
+#endif
+#ifndef FM_SELECT_STREAM_SB
+#define FM_SELECT_STREAM_SB 8     // loads per thread in flight in each streaming pass
+#endif
+
 namespace fm {
 namespace {
 
@@ -63,10 +70,23 @@ __global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
     const int64_t L = a.seg_off[s + 1] - r0;
     const double* src = a.cols + (int64_t)c * a.col_stride + r0;
     const uint8_t* msk = a.mask ? a.mask + r0 : nullptr;
+    // every pass streams the unit with SB loads per thread in flight (clamped, unconditional:
+    // a load per loop iteration would wait out one memory round trip per value)
+    constexpr int SB = FM_SELECT_STREAM_SB;
     auto for_each = [&](auto&& f) {
-        for (int64_t i = threadIdx.x; i < L; i += ST) {
-            const double x = src[i];
-            f((msk == nullptr || msk[i] != 0) ? x : NAN);
+        for (int64_t i0 = threadIdx.x; i0 < L; i0 += (int64_t)SB * ST) {
+            double xs[SB];
+            uint8_t ms[SB];
+#pragma unroll
+            for (int k = 0; k < SB; ++k) {
+                const int64_t i = i0 + (int64_t)k * ST;
+                const int64_t ic = i < L ? i : L - 1;
+                xs[k] = src[ic];
+                ms[k] = msk ? msk[ic] : (uint8_t)1;
+            }
+#pragma unroll
+            for (int k = 0; k < SB; ++k)
+                if (i0 + (int64_t)k * ST < L) f(ms[k] != 0 ? xs[k] : NAN);
         }
     };
     int cnt = 0;
@@ -663,8 +683,10 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
               x.min_count, x.lerp_mode,  x.lo,    x.hi,     x.nvalid, x.mean, x.sd,  x.center};
     hipStream_t st = (hipStream_t)stream;
     const int vpt = (max_seg_len + ST - 1) / ST;
-    if (vpt > 96) {
-        // longer than the register budget: stream every unit from HBM (exact, any length)
+    if (vpt > FM_SELECT_STREAM_VPT) {
+        // past the wave paths' register budget: stream every unit from HBM / L2 (exact, any
+        // length).  Beyond 24 values per thread the register-resident workgroup kernel runs
+        // at 1-2 waves per SIMD (spilling at 96), the streaming one at 4.
         hipLaunchKernelGGL(select_stream_kernel, dim3(nseg, ncols), dim3(ST), 0, st, a);
         FM_CHECK_LAUNCH("fm_select_cuts(stream)");
         return FM_OK;

@@ -1,1 +1,1 @@
-tools/gpu_steps.sh "kb1:::300:::python tools/kbench.py" "kb2:::300:::FM_GRAM_TARGET_CHUNKS=1200 python tools/kbench.py build_variants/gt128/libfm_hip.so" "kb3:::300:::FM_GRAM_TARGET_CHUNKS=1800 python tools/kbench.py build_variants/gt128/libfm_hip.so"
+tools/gpu_steps.sh "parity:::500:::python -u -m pytest tests/test_gpu_parity.py -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread" "bench:::400:::python bench.py --steps 20"
