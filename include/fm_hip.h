@@ -49,6 +49,8 @@
  *                      min_periods=100).std() * sqrt(252) (src/calc_Lewellen_2014.py:448-456)
  *   fm_rolling_beta <- calculate_rolling_beta's polars 156-week group_by_dynamic beta
  *                      (src/calc_Lewellen_2014.py:344-434)
+ *   fm_ffill_expand <- expand_compustat_annual_to_monthly's per-gvkey monthly reindex +
+ *                      forward fill (src/transform_compustat.py:101-172)
  *   fm_gen_panel    <- (bench/test data) counter-based synthetic panel, bit-identical to
  *                      fmcore/synth.py
  *
@@ -388,6 +390,17 @@ int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
                  double* me, uint8_t* nyse, void* stream);
 
 int fm_stream_probe(const double* src, int64_t n, double* out, void* stream);
+
+/* fm_ffill_expand: records sorted by (group, month code) with CSR rec_off[ngroups+1];
+ * out_off[ngroups+1] is the prefix of each group's output month count (planned by the
+ * caller: from its first record month to its last output month).  Output row i of group g
+ * is month rec_month[rec_off[g]] + (i - out_off[g]); it takes the group's last record with
+ * rec_month <= that month: out_src[i] = that record, out_month[i] = the month, and the
+ * ncols FP64 columns vals[c * v_stride + record] are gathered to out_vals[c * o_stride + i]. */
+int fm_ffill_expand(const int64_t* rec_off, const int32_t* rec_month, const int64_t* out_off,
+                    int32_t ngroups, int64_t nout, const double* vals, int64_t v_stride,
+                    int32_t ncols, double* out_vals, int64_t o_stride, int32_t* out_month,
+                    int64_t* out_src, void* stream);
 
 #ifdef __cplusplus
 }

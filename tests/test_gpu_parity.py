@@ -960,3 +960,53 @@ def test_rolling_beta_vs_oracle(CL):
     assert np.array_equal(got["permno"].values, exp["permno"].values)
     assert np.isfinite(exp["beta"].values).sum() > 500
     assert_series_close(got["beta"].values, exp["beta"].values, "beta")
+
+
+# ---------------------------------------------------------------- §8(f) row 3: panel ETL
+def _etl_frame_equal(got, g):
+    assert list(got.columns) == [str(c) for c in g["out_columns"]]
+    for c in got.columns:
+        a = got[c].to_numpy()
+        if c == "gvkey":
+            a = a.astype(np.int64)
+        elif np.issubdtype(got[c].dtype, np.datetime64):
+            a = got[c].to_numpy(dtype="datetime64[ns]").astype(np.int64)
+        b = g["out_" + c] if isinstance(g, dict) or hasattr(g, "files") else g[c]
+        assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), c
+
+
+def test_expand_compustat_golden():
+    """Drop-in expand_compustat_annual_to_monthly (fm_ffill_expand) against the reference's
+    own output (tests/golden/etl.npz): 40 gvkeys, 1..12 annual records with multi-year gaps,
+    the 12-month extension clipped at the table's last report date, one group with
+    mid-month report dates, NaN values, an int column -- every column exact."""
+    import etl_cases
+    import transform_compustat as TC
+    got = TC.expand_compustat_annual_to_monthly(etl_cases.comp_annual())
+    _etl_frame_equal(got, load_npz("etl.npz"))
+
+
+def test_expand_compustat_vs_oracle_large():
+    """3,000 gvkeys x up to 30 annual records (shuffled), device vs the oracle restatement,
+    exact; duplicated (gvkey, report_date) labels raise like the reference's reindex."""
+    import transform_compustat as TC
+    from oracle import etl_oracle as X
+    rng = np.random.default_rng(17)
+    rows = []
+    for k in range(3000):
+        n = int(rng.integers(1, 31))
+        yrs = np.sort(rng.choice(np.arange(1950, 2020), size=n, replace=False))
+        fye = int(rng.integers(1, 13))
+        dd = pd.to_datetime({"year": yrs, "month": np.full(n, fye), "day": np.ones(n, int)}) + pd.offsets.MonthEnd(0)
+        rows.append(pd.DataFrame({"gvkey": f"{k:06d}", "datadate": dd, "fyear": yrs,
+                                  "report_date": dd + pd.offsets.MonthEnd(4),
+                                  "be": rng.standard_normal(n), "at": rng.standard_normal(n)}))
+    df = pd.concat(rows, ignore_index=True)
+    df = df.iloc[rng.permutation(len(df))].reset_index(drop=True)
+    got = TC.expand_compustat_annual_to_monthly(df)
+    exp = X.expand_compustat_annual_to_monthly(df)
+    assert list(got.columns) == list(exp.columns) and len(got) == len(exp)
+    for c in got.columns:
+        assert np.array_equal(got[c].to_numpy(), exp[c].to_numpy()), c
+    with pytest.raises(ValueError):
+        TC.expand_compustat_annual_to_monthly(pd.concat([df, df.iloc[:1]], ignore_index=True))
