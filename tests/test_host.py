@@ -205,3 +205,16 @@ def test_month_segments_radix_order_is_stable_order():
         _, u1, o1, s1 = engine.month_segments(labels)
         np.testing.assert_array_equal(o1, ref)
         assert s1[-1] == len(ref) and len(u1) == len(uniq)
+
+
+def test_etl_month_codes_round_trip():
+    """fmcore.etl's host planning: month codes of month-end and mid-month dates, and the
+    month-end dates of codes (the calendar side of fm_ffill_expand)."""
+    import pandas as pd
+    from fmcore import etl as X
+    d = pd.to_datetime(["1964-01-31", "1999-12-31", "2000-02-29", "2013-06-15", "1970-01-01"])
+    c = X.month_code(d.to_numpy())
+    assert list(c) == [1964 * 12, 1999 * 12 + 11, 2000 * 12 + 1, 2013 * 12 + 5, 1970 * 12]
+    back = pd.DatetimeIndex(X.code_to_month_end(c))
+    assert list(back.strftime("%Y-%m-%d")) == ["1964-01-31", "1999-12-31", "2000-02-29", "2013-06-30",
+                                               "1970-01-31"]
