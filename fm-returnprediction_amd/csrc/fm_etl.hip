@@ -51,8 +51,57 @@ __global__ __launch_bounds__(XT) void ffill_expand_kernel(const int64_t* __restr
     }
 }
 
+// Equality join on a two-part int64 key (merge_CRSP_and_Compustat's gvkey and (permno,
+// jdate) merges, reference src/transform_compustat.py:218-225): right keys sorted
+// lexicographically (stable, so equal keys keep the right frame's order), one thread per left
+// row, lower / upper bound by binary search.  Matches of left row i are right rows
+// [lo[i], hi[i]) of the sorted order, i.e. pandas' merge order (left rows in order, each
+// with its matches in right order).
+__device__ __forceinline__ bool key_lt(int64_t a1, int64_t a2, int64_t b1, int64_t b2) {
+    return a1 < b1 || (a1 == b1 && a2 < b2);
+}
+
+__global__ __launch_bounds__(XT) void sorted_join_kernel(const int64_t* __restrict__ lk1,
+                                                         const int64_t* __restrict__ lk2, int64_t nl,
+                                                         const int64_t* __restrict__ rk1,
+                                                         const int64_t* __restrict__ rk2, int64_t nr,
+                                                         int64_t* __restrict__ lo, int64_t* __restrict__ hi) {
+    for (int64_t i = (int64_t)blockIdx.x * XT + threadIdx.x; i < nl; i += (int64_t)gridDim.x * XT) {
+        const int64_t k1 = lk1[i], k2 = lk2 ? lk2[i] : 0;
+        int64_t a = 0, b = nr;   // first right key >= (k1, k2)
+        while (a < b) {
+            const int64_t mid = (a + b) >> 1;
+            if (key_lt(rk1[mid], rk2 ? rk2[mid] : 0, k1, k2)) a = mid + 1;
+            else b = mid;
+        }
+        int64_t c = a, d = nr;   // first right key > (k1, k2)
+        while (c < d) {
+            const int64_t mid = (c + d) >> 1;
+            if (!key_lt(k1, k2, rk1[mid], rk2 ? rk2[mid] : 0)) c = mid + 1;
+            else d = mid;
+        }
+        lo[i] = a;
+        hi[i] = c;
+    }
+}
+
 }  // namespace
 }  // namespace fm
+
+extern "C" int fm_sorted_join(const int64_t* lk1, const int64_t* lk2, int64_t nl, const int64_t* rk1,
+                              const int64_t* rk2, int64_t nr, int64_t* lo, int64_t* hi, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(lk1 && rk1 && lo && hi, "fm_sorted_join: null pointer");
+    FM_REQUIRE((lk2 == nullptr) == (rk2 == nullptr), "fm_sorted_join: second key parts must both be set or NULL");
+    FM_REQUIRE(nl >= 0 && nr >= 0, "fm_sorted_join: bad sizes");
+    if (nl == 0) return FM_OK;
+    const int64_t blocks = (nl + XT - 1) / XT;
+    const int grid = (int)(blocks < 65535 * 16 ? blocks : 65535 * 16);
+    hipLaunchKernelGGL(sorted_join_kernel, dim3(grid), dim3(XT), 0, (hipStream_t)stream, lk1, lk2, nl, rk1, rk2,
+                       nr, lo, hi);
+    FM_CHECK_LAUNCH("fm_sorted_join");
+    return FM_OK;
+}
 
 extern "C" int fm_ffill_expand(const int64_t* rec_off, const int32_t* rec_month, const int64_t* out_off,
                                int32_t ngroups, int64_t nout, const double* vals, int64_t v_stride,

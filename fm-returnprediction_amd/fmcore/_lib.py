@@ -107,6 +107,7 @@ _SIGS = {
     "fm_standardize": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_universe_level": (_i32, [_p, _p, _i32, _i64, _p, _p, _p, _p]),
     "fm_universe": (_i32, [_p, _p, _p, _i32, _i32, _f64, _f64, _p, _p, _p, _p]),
+    "fm_sorted_join": (_i32, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     "fm_ffill_expand": (_i32, [_p, _p, _p, _i32, _i64, _p, _i64, _i32, _p, _i64, _p, _p, _p]),
     "fm_pilot_shift": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p]),
     "fm_gram": (_i32, [C.POINTER(GramArgs), _p]),

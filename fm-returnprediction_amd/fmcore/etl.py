@@ -75,3 +75,30 @@ def expand_monthly(group_codes, dates, float_cols, extend_months=12, device=None
     cols = [out_vals[c, :m].cpu().numpy() for c in range(C)]
     out_group = np.repeat(gs[starts], counts)
     return out_group, code_to_month_end(months), cols, order[src_sorted]
+
+
+def join_pairs(left_keys, right_keys, device=None):
+    """Equality join on one- or two-part int64 keys (fm_sorted_join): returns (li, rj) index
+    arrays into the left and right frames, in pandas merge order -- left rows in order, each
+    with its matches in the right frame's order."""
+    device = device or E.require_device()
+    lk = [np.ascontiguousarray(k, dtype=np.int64) for k in left_keys]
+    rk = [np.ascontiguousarray(k, dtype=np.int64) for k in right_keys]
+    nl, nr = len(lk[0]), len(rk[0])
+    if nl == 0 or nr == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    order = np.lexsort(tuple(reversed(rk)))   # stable: equal keys keep the right order
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+    dl = [t(k) for k in lk]
+    dr = [t(k[order]) for k in rk]
+    lo = torch.empty(nl, dtype=torch.int64, device=device)
+    hi = torch.empty_like(lo)
+    two = len(lk) == 2
+    L.call("fm_sorted_join", dl[0].data_ptr(), dl[1].data_ptr() if two else None, nl, dr[0].data_ptr(),
+           dr[1].data_ptr() if two else None, nr, lo.data_ptr(), hi.data_ptr(), E._stream())
+    lo, hi = lo.cpu().numpy(), hi.cpu().numpy()
+    cnt = hi - lo
+    li = np.repeat(np.arange(nl, dtype=np.int64), cnt)
+    start = np.repeat(lo - (np.cumsum(cnt) - cnt), cnt)
+    rj = order[start + np.arange(len(li), dtype=np.int64)]
+    return li, rj

@@ -51,6 +51,8 @@
  *                      (src/calc_Lewellen_2014.py:344-434)
  *   fm_ffill_expand <- expand_compustat_annual_to_monthly's per-gvkey monthly reindex +
  *                      forward fill (src/transform_compustat.py:101-172)
+ *   fm_sorted_join  <- merge_CRSP_and_Compustat's gvkey and (permno, jdate) equality merges
+ *                      (src/transform_compustat.py:218-225)
  *   fm_gen_panel    <- (bench/test data) counter-based synthetic panel, bit-identical to
  *                      fmcore/synth.py
  *
@@ -401,6 +403,12 @@ int fm_ffill_expand(const int64_t* rec_off, const int32_t* rec_month, const int6
                     int32_t ngroups, int64_t nout, const double* vals, int64_t v_stride,
                     int32_t ncols, double* out_vals, int64_t o_stride, int32_t* out_month,
                     int64_t* out_src, void* stream);
+
+/* fm_sorted_join: for each left key (lk1[i], lk2[i]) the range [lo[i], hi[i]) of equal keys
+ * in the right keys (rk1, rk2), sorted lexicographically (stably: equal keys in the right
+ * frame's order).  lk2 / rk2 may both be NULL (one-part key). */
+int fm_sorted_join(const int64_t* lk1, const int64_t* lk2, int64_t nl, const int64_t* rk1,
+                   const int64_t* rk2, int64_t nr, int64_t* lo, int64_t* hi, void* stream);
 
 #ifdef __cplusplus
 }

@@ -33,3 +33,17 @@ def expand_compustat_annual_to_monthly(comp_annual, id_col="gvkey", report_date_
     out = pd.concat(parts, ignore_index=True)
     cols = [id_col, "fund_date"] + [c for c in df.columns if c not in (id_col, "fund_date")]
     return out[cols]
+
+
+def merge_CRSP_and_Compustat(crsp, comp, ccm):
+    """Restatement of reference src/transform_compustat.py:175-226 with pandas' own merges:
+    open-ended links (NaT linkenddt) end today (:218), the gvkey left merge (:220), the link
+    window jdate in [linkdt, linkenddt] (:222), columns permno + comp's (:224-225), the inner
+    (permno, jdate) merge with CRSP (:228)."""
+    ccm = ccm.copy()
+    ccm["linkenddt"] = ccm["linkenddt"].fillna(pd.to_datetime("today"))
+    comp = comp.rename(columns={"fund_date": "jdate"})
+    m = pd.merge(comp, ccm, how="left", on=["gvkey"])
+    m = m[(m["jdate"] >= m["linkdt"]) & (m["jdate"] <= m["linkenddt"])]
+    m = m[["permno"] + list(comp.columns)]
+    return pd.merge(crsp, m, how="inner", on=["permno", "jdate"])

@@ -26,3 +26,55 @@ def comp_annual(seed=31):
                          "count": int(rng.integers(0, 40))})
     df = pd.DataFrame(rows)
     return df.iloc[rng.permutation(len(df))].reset_index(drop=True)
+
+
+def link_inputs(comp_monthly, seed=32):
+    """CRSP monthly rows, and a CCM link table for comp_monthly's gvkeys: one or two links per
+    gvkey over different windows (some open-ended: NaT linkenddt), one gvkey with no link,
+    one permno linked to two gvkeys over time; CRSP carries an overlapping column name
+    ('datadate') to exercise the _x / _y suffixes."""
+    rng = np.random.default_rng(seed)
+    gvs = sorted(comp_monthly["gvkey"].unique())
+    links = []
+    for k, gv in enumerate(gvs):
+        if k == 3:
+            continue                                    # no link: dropped by the window filter
+        permno = 10000 + k if k != 7 else 10000 + 6     # permno 10006 linked to two gvkeys
+        d = comp_monthly.loc[comp_monthly["gvkey"] == gv, "fund_date"]
+        lo, hi = d.min(), d.max()
+        mid = lo + (hi - lo) / 2
+        if rng.random() < 0.5:
+            links.append({"gvkey": gv, "permno": permno, "linkdt": lo - pd.Timedelta(days=40),
+                          "linkenddt": pd.NaT if rng.random() < 0.5 else mid})
+        else:
+            links.append({"gvkey": gv, "permno": permno, "linkdt": lo, "linkenddt": mid})
+            links.append({"gvkey": gv, "permno": permno + 500, "linkdt": mid + pd.Timedelta(days=1),
+                          "linkenddt": pd.NaT})
+    ccm = pd.DataFrame(links)
+    ccm = ccm.iloc[rng.permutation(len(ccm))].reset_index(drop=True)
+    months = pd.date_range("1959-01-31", "2045-12-31", freq="ME")
+    rows = []
+    for p in sorted(set(ccm["permno"])):
+        sel = months[rng.random(len(months)) < 0.6]
+        rows.append(pd.DataFrame({"permno": p, "jdate": sel, "me": rng.random(len(sel)) * 1e3,
+                                  "retx": rng.standard_normal(len(sel)) * 0.1,
+                                  "datadate": sel - pd.Timedelta(days=1)}))
+    crsp = pd.concat(rows, ignore_index=True)
+    crsp = crsp.iloc[rng.permutation(len(crsp))].reset_index(drop=True)
+    return crsp, ccm
+
+
+def frame_from_golden(g, prefix, datetime_cols, gvkey=True):
+    """Rebuild a frame stored by gen_etl_goldens.arrays (gvkey back to 6-digit strings,
+    int64 ns back to datetime64, NaT included)."""
+    cols = [k[len(prefix):] for k in g.files if k.startswith(prefix) and k != prefix + "columns"
+            and k != prefix + "dtypes"]
+    out = {}
+    for c in cols:
+        v = g[prefix + c]
+        if c == "gvkey" and gvkey:
+            v = np.array([f"{int(x):06d}" for x in v], dtype=object)
+        elif c in datetime_cols:
+            v = v.astype("datetime64[ns]")
+        out[c] = v
+    return pd.DataFrame(out)

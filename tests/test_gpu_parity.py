@@ -1010,3 +1010,28 @@ def test_expand_compustat_vs_oracle_large():
         assert np.array_equal(got[c].to_numpy(), exp[c].to_numpy()), c
     with pytest.raises(ValueError):
         TC.expand_compustat_annual_to_monthly(pd.concat([df, df.iloc[:1]], ignore_index=True))
+
+
+def test_merge_crsp_compustat_golden():
+    """Drop-in merge_CRSP_and_Compustat (device joins, fm_sorted_join) against the
+    reference's own output (tests/golden/etl_merge.npz): one- and two-link gvkeys, open-ended
+    links, an unlinked gvkey, a permno linked to two gvkeys, _x / _y suffixes -- columns,
+    dtypes and every value in order; the caller's ccm gets its NaT linkenddt filled, as the
+    reference does."""
+    import etl_cases
+    import transform_compustat as TC
+    g = load_npz("etl_merge.npz")
+    comp = TC.expand_compustat_annual_to_monthly(etl_cases.comp_annual())
+    crsp = etl_cases.frame_from_golden(g, "crsp_", {"jdate", "datadate"})
+    ccm = etl_cases.frame_from_golden(g, "ccm_", {"linkdt", "linkenddt"})
+    out = TC.merge_CRSP_and_Compustat(crsp, comp, ccm)
+    assert not ccm["linkenddt"].isna().any()
+    assert list(out.columns) == [str(c) for c in g["out_columns"]]
+    assert [str(t) for t in out.dtypes] == [str(t) for t in g["out_dtypes"]]
+    for c in out.columns:
+        a = out[c].to_numpy()
+        if c == "gvkey":
+            a = a.astype(np.int64)
+        elif np.issubdtype(out[c].dtype, np.datetime64):
+            a = out[c].to_numpy(dtype="datetime64[ns]").astype(np.int64)
+        assert np.array_equal(a, g["out_" + c], equal_nan=a.dtype.kind == "f"), c
