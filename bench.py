@@ -18,7 +18,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "fm-returnprediction_amd")
-for _p in (PKG, os.path.join(PKG, "src"), ROOT):
+for _p in (PKG, ROOT):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 

@@ -21,23 +21,18 @@ Firm-axis characteristic builders (§8(f) row 2; one fused device pass, fm_firm_
 Data pulls and LaTeX output of the reference are outside this drop-in (scope).
 """
 import os
-import sys
 from pathlib import Path
 from typing import Union
 
 import numpy as np
 import pandas as pd
 
-_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-if _PKG not in sys.path:
-    sys.path.insert(0, _PKG)
+from fmcore import _lib as _L
+from fmcore import api as _api
+from fmcore import engine as _E
+from fmcore import lewellen as _LW
 
-from fmcore import _lib as _L  # noqa: E402
-from fmcore import api as _api  # noqa: E402
-from fmcore import engine as _E  # noqa: E402
-from fmcore import lewellen as _LW  # noqa: E402
-
-from regressions import fama_macbeth_summary, run_monthly_cs_regressions  # noqa: E402,F401
+from .regressions import fama_macbeth_summary, run_monthly_cs_regressions  # noqa: F401
 
 OUTPUT_DIR = Path(os.environ.get("OUTPUT_DIR", "_output"))
 

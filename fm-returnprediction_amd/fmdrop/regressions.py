@@ -5,18 +5,12 @@ BaileyMeche/FM-ReturnPrediction src/regressions.py:9-131; the per-month OLS, the
 Newey-West errors and the time-series means run in libfm_hip kernels (fm_gram, fm_solve,
 fm_ts_summary) through ctypes.  statsmodels is not needed.
 """
-import os
-import sys
 
 import numpy as np
 import pandas as pd
 
-_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-if _PKG not in sys.path:
-    sys.path.insert(0, _PKG)
-
-from fmcore import api as _api  # noqa: E402
-from fmcore import engine as _E  # noqa: E402
+from fmcore import api as _api
+from fmcore import engine as _E
 
 MissingDataError = _api.MissingDataError
 

@@ -19,18 +19,11 @@ codes of the keys; the frames are assembled from the matched row indices.
 """
 from __future__ import annotations
 
-import os
-import sys
 
 import numpy as np
 import pandas as pd
 
-_HERE = os.path.dirname(os.path.abspath(__file__))
-_PKG = os.path.dirname(_HERE)
-if _PKG not in sys.path:
-    sys.path.insert(0, _PKG)
-
-from fmcore import etl as _X  # noqa: E402
+from fmcore import etl as _X
 
 
 def expand_compustat_annual_to_monthly(comp_annual: pd.DataFrame, id_col: str = "gvkey",

@@ -5,7 +5,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "fm-returnprediction_amd")
-for p in (ROOT, PKG, os.path.join(PKG, "src"), os.path.join(ROOT, "tests", "golden")):
+for p in (ROOT, PKG, os.path.join(ROOT, "tests", "golden")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

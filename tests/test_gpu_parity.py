@@ -26,13 +26,13 @@ def E():
 
 @pytest.fixture(scope="module")
 def R():
-    import regressions
+    from fmdrop import regressions
     return regressions
 
 
 @pytest.fixture(scope="module")
 def CL():
-    import calc_Lewellen_2014
+    from fmdrop import calc_Lewellen_2014
     return calc_Lewellen_2014
 
 
@@ -981,7 +981,7 @@ def test_expand_compustat_golden():
     the 12-month extension clipped at the table's last report date, one group with
     mid-month report dates, NaN values, an int column -- every column exact."""
     import etl_cases
-    import transform_compustat as TC
+    from fmdrop import transform_compustat as TC
     got = TC.expand_compustat_annual_to_monthly(etl_cases.comp_annual())
     _etl_frame_equal(got, load_npz("etl.npz"))
 
@@ -989,7 +989,7 @@ def test_expand_compustat_golden():
 def test_expand_compustat_vs_oracle_large():
     """3,000 gvkeys x up to 30 annual records (shuffled), device vs the oracle restatement,
     exact; duplicated (gvkey, report_date) labels raise like the reference's reindex."""
-    import transform_compustat as TC
+    from fmdrop import transform_compustat as TC
     from oracle import etl_oracle as X
     rng = np.random.default_rng(17)
     rows = []
@@ -1019,7 +1019,7 @@ def test_merge_crsp_compustat_golden():
     dtypes and every value in order; the caller's ccm gets its NaT linkenddt filled, as the
     reference does."""
     import etl_cases
-    import transform_compustat as TC
+    from fmdrop import transform_compustat as TC
     g = load_npz("etl_merge.npz")
     comp = TC.expand_compustat_annual_to_monthly(etl_cases.comp_annual())
     crsp = etl_cases.frame_from_golden(g, "crsp_", {"jdate", "datadate"})

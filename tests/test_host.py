@@ -111,12 +111,10 @@ def test_synth_deterministic_and_month_major():
 
 def test_table2_formatting_matches_golden_from_oracle_stats():
     """The host-side Table-2 string layout (no compute) against the reference's strings."""
-    import sys
-    sys.path.insert(0, os.path.join(ROOT, "fm-returnprediction_amd", "src"))
     import cases
     from fmtol import frame_from, load_json, load_npz
     from oracle import fm_oracle as O
-    import calc_Lewellen_2014 as CL
+    from fmdrop import calc_Lewellen_2014 as CL
     g = load_npz("fm.npz")
     meta = load_json("fm.json")
     df = frame_from(g, "in_")
