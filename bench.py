@@ -189,18 +189,12 @@ def main():
     kern = {}
     for tag in timer.names():
         kern[tag] = timer.avg_ms(tag)   # events around each eager launch (incl. launch gaps)
-    fused = "fm_month_pass" in E.LAST_LAUNCH
-    tags = (("fm_month_pass",) if fused else ("fm_select_cuts", "fm_gram")) + \
-        ("fm_universe", "fm_solve", "fm_ts_fused", "fm_ts_fused[pred]")
+    tags = ("fm_select_cuts", "fm_gram", "fm_universe", "fm_solve", "fm_ts_fused", "fm_ts_fused[pred]")
     dev_ms = {t: E.time_launch(t) for t in tags if t in E.LAST_LAUNCH}
     # algorithmic HBM bytes per launch: every panel column once (8 B per
     # value), the universe level byte, and the month tables written (cuts, pivots, Gram
     # partials); fm_select alone reads the columns only
-    T_l = panel.nseg
     cand = {"fm_select_cuts": rows_local * C * 8, "fm_gram": rows_local * (C * 8 + 1)}
-    if fused:
-        partial = E.LAST_LAUNCH["fm_month_pass"][2][2]          # [T, buckets, 136] Gram partials
-        cand["fm_month_pass"] = rows_local * (C * 8 + 1) + T_l * C * (3 * 8 + 4) + partial.numel() * 8
     dom = max((t for t in cand if t in dev_ms), key=lambda k: dev_ms[k])
     dom_ms = dev_ms[dom]
     achieved = cand[dom] / (dom_ms * 1e-3) / 1e9

@@ -1,5 +1,4 @@
-// Device-side Gram accumulation shared by fm_gram (one workgroup per month chunk) and
-// fm_month_pass (cuts + Gram of a whole month in one workgroup).
+// Device-side Gram accumulation of fm_gram (one workgroup per month chunk).
 //
 // Per wave, 64-row tiles (one row per lane):
 //   1. ncols coalesced FP64 loads per row (SoA; the next tile's loads are in flight while

@@ -1,8 +1,7 @@
-// Device-side building blocks of the exact order-statistic selection (fm_select,
-// fm_month_pass): order-preserving keys, wave bitonic sorts over DPP / permlane exchanges,
-// the exact MSB radix select, the workgroup tail selection and the numpy / pandas
-// interpolation.  Included by fm_select.hip and fm_month.hip (anonymous namespace: each
-// translation unit gets its own copy).  Compiled with -ffp-contract=off (exact lerps).
+// Device-side building blocks of the exact order-statistic selection (fm_select):
+// order-preserving keys, wave bitonic sorts over DPP / permlane exchanges, the exact MSB
+// radix select, the workgroup tail selection and the numpy / pandas interpolation
+// (anonymous namespace: each including translation unit gets its own copy).  Compiled with -ffp-contract=off (exact lerps).
 #pragma once
 #include <math.h>
 

@@ -45,16 +45,6 @@ class GramArgs(C.Structure):
     ]
 
 
-FM_MONTH_MAX_ROWS = 6144
-
-
-class MonthArgs(C.Structure):
-    _fields_ = [
-        ("gram", GramArgs), ("q_lo", _f64), ("q_hi", _f64), ("min_count", _i32),
-        ("max_seg_len", _i32), ("lo", _p), ("hi", _p), ("nvalid", _p), ("center", _p),
-    ]
-
-
 class SelectArgs(C.Structure):
     _fields_ = [
         ("cols", _p), ("col_stride", _i64), ("ncols", _i32), ("seg_off", _p), ("nseg", _i32),
@@ -111,7 +101,6 @@ _SIGS = {
     "fm_ffill_expand": (_i32, [_p, _p, _p, _i32, _i64, _p, _i64, _i32, _p, _i64, _p, _p, _p]),
     "fm_pilot_shift": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p]),
     "fm_gram": (_i32, [C.POINTER(GramArgs), _p]),
-    "fm_month_pass": (_i32, [C.POINTER(MonthArgs), _p]),
     "fm_solve": (_i32, [C.POINTER(SolveArgs), _p]),
     "fm_const_check": (_i32, [_p, _i64, _i32, _p, _i32, _p, _p, _p, _i32, _p, _p, _p, _p,
                               _i32, _p, _p]),

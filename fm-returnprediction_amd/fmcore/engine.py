@@ -585,54 +585,6 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
                     mom_stride=mom_stride)
 
 
-def month_pass_fits(panel: DevicePanel, models: Sequence[Model], nlevels=1):
-    """Whether fm_month_pass can take this pass (<= 15 columns, one model group of <= 16
-    buckets, months of <= FM_MONTH_MAX_ROWS rows); else select_cuts + fm_pass."""
-    if panel.ncols > 15 or panel.max_seg_len > L.FM_MONTH_MAX_ROWS:
-        return False
-    if len(models) > L.FM_MAX_MODELS:
-        return False
-    return len(plan_patterns(models)[1]) * nlevels <= 16
-
-
-def month_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, q_lo=0.01, q_hi=0.99,
-               min_count=5, moments=False, const_check=True):
-    """Winsorize cuts (numpy 'linear', pivot = midpoint of the cuts) and the batched Gram of
-    every (model, universe level) problem, one workgroup per month in ONE launch
-    (fm_month_pass: the month's rows are fetched from HBM once), then the solve and the
-    statsmodels fix-ups.  Returns (FMResult, Cuts)."""
-    src = panel.cols
-    dev = src.device
-    T, C = panel.nseg, panel.ncols
-    problems = _problems(models, nlevels)
-    pmax = max(2, max(p.K + 1 for p in problems))
-    mom_stride = 1 + (pmax + 1) + (pmax + 1) ** 2
-    (gpl,) = _group_plans(panel, models, problems, nlevels, 16, const_check, dev)
-    lo = torch.empty((C, T), dtype=torch.float64, device=dev)
-    hi = torch.empty_like(lo)
-    cen = torch.empty_like(lo)
-    nv = torch.empty((C, T), dtype=torch.int32, device=dev)
-    nb = gpl.npatterns * nlevels
-    partial = torch.empty((T, nb, 136), dtype=torch.float64, device=dev)
-    ga = L.GramArgs(
-        cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, nseg=T, seg_off=panel.seg_off.data_ptr(),
-        chunk_seg=None, chunk_row=None, nchunks=T, lo=None, hi=None, shift=None, inv_scale=None,
-        level=_ptr(level), nlevels=nlevels, model_mask=gpl.mm.data_ptr(), model_ymask=gpl.ym.data_ptr(),
-        nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(), npatterns=gpl.npatterns,
-        partial=partial.data_ptr(), flags=None)
-    ma = L.MonthArgs(gram=ga, q_lo=float(q_lo), q_hi=float(q_hi), min_count=int(min_count),
-                     max_seg_len=max(panel.max_seg_len, 1), lo=lo.data_ptr(), hi=hi.data_ptr(),
-                     nvalid=nv.data_ptr(), center=cen.data_ptr())
-    _kcall("fm_month_pass", "fm_month_pass", L.C.byref(ma), _stream())
-    _remember("fm_month_pass", "fm_month_pass", ma, src, level, partial, lo, hi, cen, nv, gpl, panel.seg_off)
-    soff = _small_tensor(tuple(range(T + 1)), torch.int32, dev)
-    rec, st, mom = _solve_group(panel, src, gpl, partial, soff, 16, nlevels, T, pmax, mom_stride, lo, hi,
-                                cen, None, cen, level, const_check, (src, lo, hi, cen, level))
-    res = FMResult(problems=problems, rec=rec, status=st, pmax=pmax, moments=mom if moments else None,
-                   mom_stride=mom_stride)
-    return res, Cuts(lo, hi, nv, center=cen)
-
-
 def drop_degenerate_months(res: FMResult, models: Sequence[Model], sd):
     """Standardized passes (A9): a month in which a regressor has fewer than two values or
     zero dispersion has an all-NaN z-score column, so every row drops out and the month is

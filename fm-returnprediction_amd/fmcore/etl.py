@@ -38,7 +38,13 @@ def expand_monthly(group_codes, dates, float_cols, extend_months=12, device=None
     src [m] int64 index into the ORIGINAL records)."""
     device = device or E.require_device()
     g = np.asarray(group_codes)
-    dates = pd.DatetimeIndex(dates)
+    # one unit for every date quantity below (Parquet / to_datetime give [us] or [s]; the
+    # 12-month clip compares against max_all.value, which is always ns)
+    dates = pd.DatetimeIndex(dates).as_unit("ns")
+    if dates.hasnans:
+        raise ValueError("report dates contain NaT")
+    if (g < 0).any():
+        raise ValueError("group codes must be >= 0 (drop rows with a missing id first)")
     n = len(g)
     if n == 0:
         return g[:0], np.zeros(0, "datetime64[ns]"), [np.zeros(0) for _ in float_cols], np.zeros(0, np.int64)

@@ -72,9 +72,6 @@ class PipelineConfig:
     lag: int = 1
     forecasts: bool = True
     fig1: bool = True
-    # one launch per pass for the winsorize cuts + batched Gram (fm_month_pass) instead of
-    # fm_select + fm_gram; off by default until it is the faster of the two
-    fused_month: bool = False
 
 
 @dataclass
@@ -130,17 +127,6 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
     level, bp = None, None
     nlevels = 1
     models, names = build_models(panel, model_cols, y=y, fig1=cfg.fig1, universes=cfg.universes)
-    if cfg.fused_month and cfg.winsorize and not cfg.standardize and \
-            E.month_pass_fits(panel, models, 3 if cfg.universes else 1):
-        # fused path: NYSE breakpoints + universe levels, then ONE launch per pass doing the
-        # winsorize cuts and the batched Gram month by month (fm_month_pass)
-        if cfg.universes:
-            a, b, level = E.universe(panel)
-            nlevels = 3
-            bp = (a, b)
-        res, cuts = E.month_pass(panel, models, level=level, nlevels=nlevels, q_lo=cfg.lower_percentile / 100,
-                                 q_hi=cfg.upper_percentile / 100, min_count=5, moments=cfg.forecasts)
-        return res, names, cuts, level, bp
     if cfg.universes:
         # one launch, on the pass's own stream: a side-stream fork / join inside the captured
         # graph cost more in cross-queue synchronization than the overlap saved

@@ -5,7 +5,9 @@ expand_compustat_annual_to_monthly keeps the reference's name, signature and out
 month-end from its first `report_date` to min(the table's latest report date, its own last
 report date + 12 months), each carrying the group's latest record at or before that month
 (pandas reindex(method="ffill")), columns [id_col, "fund_date", <the input columns except
-fyear>], sorted by (id_col, fund_date).  The forward-fill gather runs on the device
+fyear>], sorted by (id_col, fund_date); fund_date is datetime64[ns] whatever the input unit
+(pd.date_range's default), rows with a missing id are dropped (groupby), a NaT report date
+raises ValueError (as the reference's date_range / reindex do).  The forward-fill gather runs on the device
 (fmcore.etl.expand_monthly -> fm_ffill_expand); float64 columns are gathered there, columns
 of other dtypes by the same source indices on the host.  Like the reference (whose
 reindex raises on duplicate labels), a repeated (id, report_date) raises ValueError.
@@ -29,7 +31,12 @@ from fmcore import etl as _X
 def expand_compustat_annual_to_monthly(comp_annual: pd.DataFrame, id_col: str = "gvkey",
                                        report_date_col: str = "report_date") -> pd.DataFrame:
     df = comp_annual.drop(columns=["fyear"], errors="ignore")
+    # groupby(level=id_col) drops rows whose id is missing (reference :165-168)
+    df = df.loc[df[id_col].notna().to_numpy()]
     dates = pd.to_datetime(df[report_date_col])
+    if dates.isna().any():
+        # the reference's per-group date_range / reindex raise ValueError on a NaT date
+        raise ValueError("report_date contains NaT")
     if df.duplicated(subset=[id_col, report_date_col]).any():
         raise ValueError("cannot reindex on an axis with duplicate labels")
     codes, uniq = pd.factorize(df[id_col], sort=True)

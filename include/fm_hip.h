@@ -207,30 +207,6 @@ int fm_pilot_shift(const double* cols, int64_t col_stride, int32_t ncols,
 
 int fm_gram(const fm_gram_args* args, void* stream);
 
-/* fm_month_pass: fm_select (winsorize cuts, numpy 'linear' lerp, + the Gram pivot) AND
- * fm_gram for whole months in ONE launch, one workgroup per month: the month's rows are
- * fetched from HBM once.  Replaces np.percentile(vals, 1/99) + clip of every column
- * (src/calc_Lewellen_2014.py:519-524), dropna + universe subsetting (src/regressions.py:39;
- * src/calc_Lewellen_2014.py:95-105) and the X'X / X'y / y'y of every model x universe
- * (src/regressions.py:57; :917-919).  gram.partial is [nseg][nbuckets][136] (one chunk
- * per month: fm_solve with seg_chunk_off = 0..nseg); gram.chunk_*, lo, hi, shift and
- * inv_scale are not read (the cuts and pivots are computed here and written to lo / hi /
- * center / nvalid, [ncols][nseg]).  Limits: ncols <= 15, nbuckets <= 16, months of at most
- * FM_MONTH_MAX_ROWS rows; beyond them FM_ETOOBIG (callers use fm_select + fm_gram). */
-#define FM_MONTH_MAX_ROWS 6144
-typedef struct fm_month_args {
-    fm_gram_args gram;
-    double q_lo, q_hi;            /* winsorize quantiles in [0, 1] */
-    int32_t min_count;            /* fewer valid values: cuts are NaN (no clipping) */
-    int32_t max_seg_len;          /* longest month (rows) */
-    double* lo;                   /* [ncols][nseg] outputs */
-    double* hi;
-    int32_t* nvalid;              /* may be NULL */
-    double* center;
-} fm_month_args;
-
-int fm_month_pass(const fm_month_args* args, void* stream);
-
 int fm_solve(const fm_solve_args* args, void* stream);
 
 /* fm_const_check / fm_solve_fixup: `pairs` lists (month, problem) int32 pairs; npairs < 0

@@ -52,7 +52,10 @@ def link_inputs(comp_monthly, seed=32):
                           "linkenddt": pd.NaT})
     ccm = pd.DataFrame(links)
     ccm = ccm.iloc[rng.permutation(len(ccm))].reset_index(drop=True)
-    months = pd.date_range("1959-01-31", "2045-12-31", freq="ME")
+    # CRSP months stop before any plausible run date: the reference fills open-ended links
+    # with pd.to_datetime("today"), so merged rows past the run date would make the fixture
+    # depend on the wall clock (every jdate here is <= 2019-12 < today)
+    months = pd.date_range("1959-01-31", "2019-12-31", freq="ME")
     rows = []
     for p in sorted(set(ccm["permno"])):
         sel = months[rng.random(len(months)) < 0.6]
@@ -62,6 +65,21 @@ def link_inputs(comp_monthly, seed=32):
     crsp = pd.concat(rows, ignore_index=True)
     crsp = crsp.iloc[rng.permutation(len(crsp))].reset_index(drop=True)
     return crsp, ccm
+
+
+def unit_variants(df):
+    """The reference's expansion over inputs pandas 2 produces from Parquet / to_datetime:
+    report dates in datetime64[us] and [s], and a frame with missing gvkeys (groupby drops
+    them).  {name: frame}."""
+    out = {}
+    for unit in ("us", "s"):
+        d = df.copy()
+        d["report_date"] = d["report_date"].astype(f"datetime64[{unit}]")
+        out[unit] = d
+    d = df.copy()
+    d.loc[d.index[::17], "gvkey"] = None
+    out["nakey"] = d
+    return out
 
 
 def frame_from_golden(g, prefix, datetime_cols, gvkey=True):
@@ -78,3 +96,17 @@ def frame_from_golden(g, prefix, datetime_cols, gvkey=True):
             v = v.astype("datetime64[ns]")
         out[c] = v
     return pd.DataFrame(out)
+
+
+def assert_frame_matches(out, g, prefix):
+    """Columns, dtypes (when stored) and every value of `out` against a stored frame."""
+    assert list(out.columns) == [str(c) for c in g[prefix + "columns"]]
+    if prefix + "dtypes" in g.files:
+        assert [str(t) for t in out.dtypes] == [str(t) for t in g[prefix + "dtypes"]]
+    for c in out.columns:
+        a = out[c].to_numpy()
+        if c == "gvkey":
+            a = np.array([-1 if x is None else int(x) for x in a], dtype=np.int64)
+        elif np.issubdtype(out[c].dtype, np.datetime64):
+            a = out[c].to_numpy(dtype="datetime64[ns]").astype(np.int64)
+        assert np.array_equal(a, g[prefix + c], equal_nan=a.dtype.kind == "f"), c

@@ -1035,3 +1035,20 @@ def test_merge_crsp_compustat_golden():
         elif np.issubdtype(out[c].dtype, np.datetime64):
             a = out[c].to_numpy(dtype="datetime64[ns]").astype(np.int64)
         assert np.array_equal(a, g["out_" + c], equal_nan=a.dtype.kind == "f"), c
+
+
+def test_expand_compustat_units_and_missing_ids():
+    """[us] / [s] report dates and missing gvkeys against the reference's own output
+    (etl_units.npz): the 12-month clip is computed in one unit, fund_date is
+    datetime64[ns] as the reference's date_range gives, missing ids are dropped as groupby
+    does; a NaT report date raises ValueError like the reference's reindex."""
+    import etl_cases
+    from fmdrop import transform_compustat as TC
+    g = load_npz("etl_units.npz")
+    base = etl_cases.comp_annual()
+    for name, frame in etl_cases.unit_variants(base).items():
+        etl_cases.assert_frame_matches(TC.expand_compustat_annual_to_monthly(frame), g, name + "_")
+    bad = base.copy()
+    bad.loc[3, "report_date"] = pd.NaT
+    with pytest.raises(ValueError):
+        TC.expand_compustat_annual_to_monthly(bad)

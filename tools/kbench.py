@@ -18,8 +18,7 @@ def child():
     from fmcore import lewellen as LW
     dev = E.require_device()
     panel = E.panel_synthetic(600, 5000, 1, device=dev)
-    fused = os.environ.get("KB_FUSED") == "1"
-    cfg = LW.PipelineConfig(fused_month=fused)
+    cfg = LW.PipelineConfig()
     for _ in range(3):
         LW.run_pipeline(panel, cfg)
     torch.cuda.synchronize()
