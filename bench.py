@@ -59,6 +59,7 @@ def main():
     from fmcore import dist as D
     from fmcore import engine as E
     from fmcore import lewellen as LW
+    from fmcore.step import ShardedStep
 
     cfg = LW.PipelineConfig()
     model_cols = LW.table2_models()
@@ -68,104 +69,24 @@ def main():
     # chunk the Gram by the GLOBAL panel so per-month sums are identical for any rank count
     panel.chunk_rows = E.default_chunk_rows(T_glob * N, T_glob, N)
     rows_local = T_loc * N
-    seg_lo, seg_hi = rank * T_loc, (rank + 1) * T_loc
-    counts = [T_loc] * world
-
-    # One step = three device phases (each replayed from a HIP graph: the pass is ~20 short
-    # kernels, so eager launches would leave the GPU waiting on the host) with the two RCCL
-    # exchanges of the month-sharded path between them, into static buffers.
-    rec_g = st_g = None
-
-    def phase_local():
-        res, names, cuts, level, bp = LW.local_stage(panel, cfg, model_cols)
-        return res
-
-    def phase_ts(res):
-        gres = res
-        if world > 1:
-            gres = E.FMResult(problems=res.problems, rec=rec_g, status=st_g, pmax=res.pmax,
-                              moments=res.moments, mom_stride=res.mom_stride)
-        ix, summ, roll, pred, pst = LW.time_series_stage(gres, cfg, moments=res.moments,
-                                                         seg_lo=seg_lo, seg_hi=seg_hi)
-        return gres, summ, pred, pst
-
-    def phase_pred(pred, pst):
-        psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
-        return psumm
-
-    def exchange_records(res):
-        if world > 1:
-            D.gather_records_into(res.rec, res.status, rec_g, st_g)
-
-    def exchange_pred(pred, pst):
-        if world > 1:
-            D.combine_predictive(pred, pst)
-
-    def step_eager():
-        res = phase_local()
-        exchange_records(res)
-        gres, summ, pred, pst = phase_ts(res)
-        exchange_pred(pred, pst)
-        return gres, summ, phase_pred(pred, pst)
-
-    for _ in range(args.warmup):
-        res0 = phase_local()
-        if world > 1 and rec_g is None:
-            rec_g = torch.empty((T_glob,) + tuple(res0.rec.shape[1:]), dtype=res0.rec.dtype, device=dev)
-            st_g = torch.empty((T_glob,) + tuple(res0.status.shape[1:]), dtype=res0.status.dtype, device=dev)
-        exchange_records(res0)
-        g0, s0, p0, ps0 = phase_ts(res0)
-        exchange_pred(p0, ps0)
-        phase_pred(p0, ps0)
+    step = ShardedStep(panel, cfg, model_cols, world=world, rank=rank, seg_lo=rank * T_loc,
+                       seg_hi=(rank + 1) * T_loc, global_months=T_glob, counts=[T_loc] * world)
+    for _ in range(max(1, args.warmup)):   # >= 1: allocates the static exchange buffers
+        step.eager()
     torch.cuda.synchronize()
-
-    graphs = None
     if not args.no_graph:
-        # capture (on a side stream, as torch.cuda.graph requires); eager warmup has filled
-        # every host-side cache, so the captured launches are exactly a step's kernels
-        if world == 1:
-            # no exchange at N=1: the whole step is one graph (no inter-graph launch gaps)
-            g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                res_s = phase_local()
-                gres_s, summ_s, pred_s, pst_s = phase_ts(res_s)
-                psumm_s = phase_pred(pred_s, pst_s)
-            graphs = (g1,)
-
-            def step():
-                g1.replay()
-                return gres_s, summ_s, psumm_s
-        else:
-            ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga):
-                res_s = phase_local()
-            exchange_records(res_s)
-            with torch.cuda.graph(gb):
-                gres_s, summ_s, pred_s, pst_s = phase_ts(res_s)
-            exchange_pred(pred_s, pst_s)
-            with torch.cuda.graph(gc):
-                psumm_s = phase_pred(pred_s, pst_s)
-            graphs = (ga, gb, gc)
-
-            def step():
-                ga.replay()
-                exchange_records(res_s)
-                gb.replay()
-                exchange_pred(pred_s, pst_s)
-                gc.replay()
-                return gres_s, summ_s, psumm_s
-    else:
-        step = step_eager
-
+        # capture (on a side stream, as torch.cuda.graph requires); the eager warm-up has
+        # filled every host-side cache, so the captured launches are exactly a step's kernels
+        step.capture()
     for _ in range(2):
-        step()
+        step.replay()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = step()
+        out = step.replay()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -178,7 +99,7 @@ def main():
     timer = E.KernelTimer()
     with timer:
         for _ in range(max(3, min(args.steps, 10))):
-            step_eager()
+            step.eager()
     torch.cuda.synchronize()
     gres, summ, psumm = out
     nfit = int(((gres.status & 1) != 0).sum().item())

@@ -20,9 +20,6 @@
 #include "fm_common.h"
 
 // A/B and ablation knobs: timing builds only (tools/kbench.py), never the shipped library
-#ifndef FM_GRAM_PIPE
-#define FM_GRAM_PIPE 0   // 1: software-pipelined MFMA operand reads (measured slower)
-#endif
 #ifndef FM_AB_GRAM_NOMFMA
 #define FM_AB_GRAM_NOMFMA 0
 #endif
@@ -43,6 +40,16 @@ namespace {
 __device__ __forceinline__ uint32_t push_valid(uint32_t nn, double x) {
     asm("v_cmp_o_f64 vcc, %1, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(nn) : "v"(x) : "vcc");
     return nn;
+}
+
+// Lane value rotated within each 16-lane row: DPP row_ror:N gives lane i the value of lane
+// (i - N) & 15 of its row (fm_common.h xor_lanes<4> relies on the same rule).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 // 4x4 block pairs (I, J) of the ZW x ZW Gram covered by the 4x4x4 MFMAs of one 4-row group.
@@ -239,59 +246,65 @@ struct GramWave {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // ---- MFMA accumulation per bucket: NI independent 4x4x4 block products per
-            // 4-row group; in the bucket's last (partial) group the lanes of rows past the
-            // count read the zero rows instead.  Per-bucket counts are popcounts of the
-            // ballot masks, formed on the fly (scalar).
-            const double* rp = wt;
+            // 4-row group; rows past the bucket's count contribute zeros.  Per-bucket counts
+            // are popcounts of the ballot masks, formed on the fly (scalar).
             if (FM_AB_GRAM_NOMFMA) {
-                if (__popcll(bv) == 65) acc[0][0] += rp[oa[0]];   // keeps bv/dest alive
+                if (__popcll(bv) == 65) acc[0][0] += wt[oa[0]];   // keeps bv/dest alive
                 return;
             }
+            if constexpr (NT == 1) {
+                // ONE LDS read per group: lane (kr, q) reads z[row kr][q] = the A operand; the
+                // B operands z[kr][(q + 4k) & 15] are the same register of lane (kr, q + 4k),
+                // i.e. a DPP rotation within the lane's 16-lane row (row_ror 12 / 8).  The
+                // next group's read is issued before this group's MFMAs (the sorted tile is
+                // contiguous: the next group starts 4 rows on, or at the next bucket's start
+                // = this bucket's end, whatever buckets in between are empty).
+                const int abase = (lane >> 4) * RS + (lane & 15);
+                const double* rd = wt + abase;
+                double An = rd[0];
+                int off = 0;
 #pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                uint64_t mb = bv;
+                for (int b = 0; b < NB; ++b) {
+                    uint64_t mb = bv;
 #pragma unroll
-                for (int i = 0; i < KB; ++i) mb &= ((b >> i) & 1) ? bit[i] : ~bit[i];
-                const int n = (int)__popcll(mb);
-                if constexpr (NT == 1 && FM_GRAM_PIPE) {
-                    // software-pipelined: the next group's three operands (A = B0, B1, B2)
-                    // are read while this group's MFMAs run; lanes of rows past the count
-                    // read the zero rows
-                    const int ng = (n + 3) >> 2;
-                    if (ng > 0) {
-                        const double* p = kr < n ? rp : zblk;
-                        double A = p[oa[0]], B1 = p[ob[1]], B2 = p[ob[2]];
-                        for (int g = 0; g < ng; ++g) {
-                            double nA = 0.0, nB1 = 0.0, nB2 = 0.0;
-                            if (g + 1 < ng) {
-                                const double* q = 4 * (g + 1) + kr < n ? rp + 4 * (g + 1) * RS : zblk;
-                                nA = q[oa[0]];
-                                nB1 = q[ob[1]];
-                                nB2 = q[ob[2]];
-                            }
-                            acc[b][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, A, acc[b][0], 0, 0, 0);
-                            acc[b][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, B1, acc[b][1], 0, 0, 0);
-                            acc[b][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, B2, acc[b][2], 0, 0, 0);
-                            A = nA;
-                            B1 = nB1;
-                            B2 = nB2;
-                        }
-                        rp += n * RS;
+                    for (int i = 0; i < KB; ++i) mb &= ((b >> i) & 1) ? bit[i] : ~bit[i];
+                    const int n = (int)__popcll(mb);
+                    for (int g = 0; g < n; g += 4) {
+                        const double Ar = An;
+                        const int rn = g + 4 < n ? off + g + 4 : off + n;
+                        // rows past the tile end (< 3 of them: lanes of rows past a
+                        // bucket's count) read the next wave's tile or the zero rows that
+                        // follow the last one, and are masked below
+                        An = rd[rn * RS];
+                        const double A = kr < n - g ? Ar : 0.0;
+                        const double B1 = dpp_f64<0x12C>(A), B2 = dpp_f64<0x128>(A);
+                        acc[b][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, A, acc[b][0], 0, 0, 0);
+                        acc[b][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, B1, acc[b][1], 0, 0, 0);
+                        acc[b][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, B2, acc[b][2], 0, 0, 0);
                     }
-                    continue;
+                    off += n;
                 }
-                int g = 0;
-                for (; g + 4 <= n; g += 4, rp += 4 * RS) {
+            } else {
+                const double* rp = wt;
 #pragma unroll
-                    for (int k = 0; k < NI; ++k)
-                        acc[b][k] = __builtin_amdgcn_mfma_f64_4x4x4f64(rp[oa[k]], rp[ob[k]], acc[b][k], 0, 0, 0);
-                }
-                if (g < n) {
-                    const double* bp = g + kr < n ? rp : zblk;
+                for (int b = 0; b < NB; ++b) {
+                    uint64_t mb = bv;
 #pragma unroll
-                    for (int k = 0; k < NI; ++k)
-                        acc[b][k] = __builtin_amdgcn_mfma_f64_4x4x4f64(bp[oa[k]], bp[ob[k]], acc[b][k], 0, 0, 0);
-                    rp += (n - g) * RS;
+                    for (int i = 0; i < KB; ++i) mb &= ((b >> i) & 1) ? bit[i] : ~bit[i];
+                    const int n = (int)__popcll(mb);
+                    int g = 0;
+                    for (; g + 4 <= n; g += 4, rp += 4 * RS) {
+#pragma unroll
+                        for (int k = 0; k < NI; ++k)
+                            acc[b][k] = __builtin_amdgcn_mfma_f64_4x4x4f64(rp[oa[k]], rp[ob[k]], acc[b][k], 0, 0, 0);
+                    }
+                    if (g < n) {
+                        const double* bp = g + kr < n ? rp : zblk;
+#pragma unroll
+                        for (int k = 0; k < NI; ++k)
+                            acc[b][k] = __builtin_amdgcn_mfma_f64_4x4x4f64(bp[oa[k]], bp[ob[k]], acc[b][k], 0, 0, 0);
+                        rp += (n - g) * RS;
+                    }
                 }
             }
             // the next tile's scatter overwrites this tile: every operand read above has been

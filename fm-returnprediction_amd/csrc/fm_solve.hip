@@ -412,6 +412,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     // loads issued together with the partials' (read in place, each would be a dependent
     // memory round trip inside the problem loop)
     __shared__ int t_model[S16_MAXP], t_level[S16_MAXP], t_nz[S16_MAXP], t_flags[S16_MAXP];
+    __shared__ int t_slot[S16_MAXP];   // wave slot -> problem, by descending K
     __shared__ uint8_t t_z[S16_MAXP][32];
     __shared__ uint32_t t_pat[64];
     __shared__ double t_ab[32];
@@ -419,8 +420,18 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     if (tid < a.nprob) {
         t_model[tid] = a.prob_model[tid];
         t_level[tid] = a.prob_level[tid];
-        t_nz[tid] = a.prob_nz[tid];
+        const int nzp = a.prob_nz[tid];
+        t_nz[tid] = nzp;
         t_flags[tid] = a.prob_flags[tid];
+        // Problems go to wave slots by descending K (ties: index order): the factorization
+        // loops run to the largest K of the wave's four problems, so grouping similar K
+        // cuts the issued work (Table 2: 3 x K 14, 3 x 7, 2 x 5, 3 x 3 per month)
+        int rank = 0;
+        for (int q = 0; q < a.nprob; ++q) {
+            const int nzq = a.prob_nz[q];
+            rank += (nzq > nzp || (nzq == nzp && q < tid)) ? 1 : 0;
+        }
+        t_slot[rank] = tid;
     }
     if (tid < npat) t_pat[tid] = a.pattern_models[tid];
     if (a.add_back && tid >= 64 && tid < 96) {
@@ -446,9 +457,12 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     for (int p0 = w * 4; p0 < a.nprob; p0 += S16W * 4) {
         const int p = p0 + g;
         const bool live = p < a.nprob;
-        const int pp = live ? p : p0;
+        const int pp = t_slot[live ? p : p0];
         const int m = t_model[pp], u = t_level[pp], nz = t_nz[pp];
         const int K = nz - 2, K1 = K + 1;
+        // wave-uniform loop bound: the largest K of this wave's problems (slots by
+        // descending K: the first live slot's)
+        const int kw = __builtin_amdgcn_readfirstlane(K);
         const int zi = i < nz ? t_z[pp][i] : 0;   // z index of this lane's row
         // ---- row i of the problem Gram: one level-cumulative bucket per pattern with m.
         // A lambda, so the rare rank-deficient path re-reads G from LDS instead of keeping it
@@ -467,7 +481,8 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                 if (!((t_pat[q] >> m) & 1u)) continue;   // per problem
                 const double* bq = bs + (q * nl + u) * zz;
 #pragma unroll
-                for (int j = 0; j < G16; ++j) G[j] += bq[off[j]];
+                for (int j = 0; j < G16; ++j)
+                    if (j < kw + 2) G[j] += bq[off[j]];   // columns past the wave's K: unused
             }
         };
         double G[G16];
@@ -481,6 +496,10 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
             constexpr int j = decltype(jc)::value;
             if (i == j) gdiag = G[j];
             if constexpr (j + 1 < G16) {
+                if (j > kw) {   // wave-uniform: past every problem's last column
+                    row[j] = 0.0;
+                    return;
+                }
                 const double g0j = rowbc<0>(G[j + 1]);   // G[0][j+1]
                 const double v = srow && j < K1 ? G[j + 1] - G[0] * g0j / n : 0.0;
                 row[j] = v;
@@ -519,6 +538,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         bool ok = act0, illc = false;
         static_for<0, G16 - 1>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
+            if (k >= kw) return;   // wave-uniform: no problem of the wave has pivot k
             const bool act = ok && k < K;
             const double orig = rowbc<k + 1>(sii);
             const double piv = rowbc<k + 1>(row[k]);
@@ -531,6 +551,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
             const double lik = row[k] * rinv;
             static_for<k + 1, G16>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
+                if (j > kw) return;   // wave-uniform
                 const double sj = rowbc<k + 1>(row[j]) * rinv;   // L[j][k] = S(k)[k][j] / lkk
                 if (go && j <= K) row[j] -= lik * sj;
             });
@@ -555,6 +576,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         double t = (i >= 1 && i <= K) ? T[K * (G16 + 1) + rr] : 0.0;
         static_for<0, G16 - 1>([&](auto jc) {
             constexpr int j = 14 - decltype(jc)::value;   // descending
+            if (j >= kw) return;   // wave-uniform
             const double bj = rowbc<j + 1>(t) / rowbc<j + 1>(col[j]);
             if (ok && j < K) {
                 if (i == j + 1) t = bj;

@@ -33,6 +33,12 @@ def shard_bounds(seg_rows, world):
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
+def _host_staged(t, group):
+    """gloo moves host memory: device tensors are staged through host copies (the tests run
+    the sharded step as several processes on one GPU over gloo; RCCL takes device memory)."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def _gather_rows(t, counts, group=None):
     """All-gather a [T_local, ...] tensor whose first dim differs per rank."""
     world = dist.get_world_size(group)
@@ -54,7 +60,11 @@ def gather_records_into(rec, status, rec_out, status_out, counts=None, group=Non
     around the exchange can be replayed from HIP graphs).  Equal month counts per rank use
     one all_gather_into_tensor per buffer."""
     world = dist.get_world_size(group)
-    if counts is None or len(set(counts)) == 1:
+    if _host_staged(rec, group):
+        r, s = gather_records(rec.cpu(), status.cpu(), counts or [rec.shape[0]] * world, group)
+        rec_out.copy_(r)
+        status_out.copy_(s)
+    elif counts is None or len(set(counts)) == 1:
         dist.all_gather_into_tensor(rec_out, rec.contiguous(), group=group)
         dist.all_gather_into_tensor(status_out, status.contiguous(), group=group)
     else:
@@ -68,12 +78,19 @@ def gather_records_into(rec, status, rec_out, status_out, counts=None, group=Non
 def combine_predictive(pred, pst, group=None):
     """Rows of other ranks' months are zero in `pred`/`pst`: a SUM all-reduce merges them
     (each compact row has exactly one owner)."""
-    dist.all_reduce(pred, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(pst, op=dist.ReduceOp.SUM, group=group)
+    for t in (pred, pst):
+        if _host_staged(t, group):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return pred, pst
 
 
 def max_over_ranks(x, device, group=None):
+    if dist.get_backend(group) == "gloo":
+        device = torch.device("cpu")
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())

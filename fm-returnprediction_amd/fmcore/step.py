@@ -1,0 +1,119 @@
+"""One step of the month-sharded full Fama-MacBeth pass (what bench.py times).
+
+A step is three device phases with the two exchanges of SURVEY.md §8(e) between them:
+
+  phase_local   cuts, universes, batched Gram + solve of this rank's months
+  exchange 1    all-gather of the monthly records into static global buffers
+  phase_ts      time-series stage on the full series (FM means, NW, rolling means, the
+                predictive records of this rank's months)
+  exchange 2    SUM all-reduce of the predictive records (each row has one owner)
+  phase_pred    FM summary of the predictive slopes
+
+At world size 1 there is no exchange and the whole step can be replayed from ONE HIP graph;
+otherwise each phase is its own graph (static buffers), with the exchanges between replays.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import dist as D
+from . import engine as E
+from . import lewellen as LW
+
+
+class ShardedStep:
+    def __init__(self, panel: E.DevicePanel, cfg: LW.PipelineConfig, model_cols, world=1, rank=0,
+                 seg_lo=0, seg_hi=None, global_months=None, counts=None, group=None):
+        self.panel, self.cfg, self.model_cols = panel, cfg, model_cols
+        self.world, self.rank, self.group = world, rank, group
+        self.seg_lo = seg_lo
+        self.seg_hi = seg_lo + panel.nseg if seg_hi is None else seg_hi
+        self.global_months = global_months or panel.nseg * world
+        self.counts = counts
+        self.rec_g = self.st_g = None
+        self.graphs = None
+        self._out = None
+
+    # ---- phases ------------------------------------------------------------------------
+    def phase_local(self):
+        res, names, cuts, level, bp = LW.local_stage(self.panel, self.cfg, self.model_cols)
+        if self.world > 1 and self.rec_g is None:
+            dev = res.rec.device
+            self.rec_g = torch.empty((self.global_months,) + tuple(res.rec.shape[1:]), dtype=res.rec.dtype,
+                                     device=dev)
+            self.st_g = torch.empty((self.global_months,) + tuple(res.status.shape[1:]), dtype=res.status.dtype,
+                                    device=dev)
+        return res
+
+    def exchange_records(self, res):
+        if self.world > 1:
+            D.gather_records_into(res.rec, res.status, self.rec_g, self.st_g, self.counts, self.group)
+
+    def phase_ts(self, res):
+        gres = res
+        if self.world > 1:
+            gres = E.FMResult(problems=res.problems, rec=self.rec_g, status=self.st_g, pmax=res.pmax,
+                              moments=res.moments, mom_stride=res.mom_stride)
+        ix, summ, roll, pred, pst = LW.time_series_stage(gres, self.cfg, moments=res.moments,
+                                                         seg_lo=self.seg_lo, seg_hi=self.seg_hi)
+        return gres, summ, pred, pst
+
+    def exchange_pred(self, pred, pst):
+        if self.world > 1 and pred is not None:
+            D.combine_predictive(pred, pst, self.group)
+
+    def phase_pred(self, pred, pst):
+        if pred is None:
+            return None
+        psumm, _ = E.summarize_predictive(pred, pst, self.cfg.nw_lags)
+        return psumm
+
+    # ---- whole step --------------------------------------------------------------------
+    def eager(self):
+        """(global FMResult, Summary, predictive Summary) with eager launches."""
+        res = self.phase_local()
+        self.exchange_records(res)
+        gres, summ, pred, pst = self.phase_ts(res)
+        self.exchange_pred(pred, pst)
+        return gres, summ, self.phase_pred(pred, pst)
+
+    def capture(self):
+        """Capture the phases as HIP graphs (after an eager warm-up has filled every
+        host-side cache and allocated the static exchange buffers)."""
+        if self.world == 1:
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                res = self.phase_local()
+                gres, summ, pred, pst = self.phase_ts(res)
+                psumm = self.phase_pred(pred, pst)
+            self.graphs = (g1,)
+            self._out = (gres, summ, psumm)
+            self._static = None
+            return
+        ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga):
+            res = self.phase_local()
+        self.exchange_records(res)
+        with torch.cuda.graph(gb):
+            gres, summ, pred, pst = self.phase_ts(res)
+        self.exchange_pred(pred, pst)
+        with torch.cuda.graph(gc):
+            psumm = self.phase_pred(pred, pst)
+        self.graphs = (ga, gb, gc)
+        self._static = (res, pred, pst)
+        self._out = (gres, summ, psumm)
+
+    def replay(self):
+        if self.graphs is None:
+            return self.eager()
+        if self.world == 1:
+            self.graphs[0].replay()
+            return self._out
+        res, pred, pst = self._static
+        ga, gb, gc = self.graphs
+        ga.replay()
+        self.exchange_records(res)
+        gb.replay()
+        self.exchange_pred(pred, pst)
+        gc.replay()
+        return self._out

@@ -54,7 +54,20 @@ def _worker(rank, world, port, T, P, rs, q):
     tp, ts = D.combine_predictive(torch.from_numpy(pred.copy()), torch.from_numpy(pst.copy()))
     ok_pred = bool(np.array_equal(tp.numpy(), pred_full) and (ts.numpy() == 1).all())
     mx = D.max_over_ranks(float(rank + 1), torch.device("cpu"))
-    q.put((rank, ok_gather, ok_pred, mx, counts))
+    # gather_records_into (the call bench.py makes, into static global buffers): uneven
+    # counts take the padded all_gather, equal counts all_gather_into_tensor
+    r_out = torch.full((T, P, rs), np.nan, dtype=torch.float64)
+    s_out = torch.full((T, P), -7, dtype=torch.int32)
+    D.gather_records_into(torch.from_numpy(rec[s0:s1]), torch.from_numpy(st[s0:s1]), r_out, s_out, counts)
+    ok_into = bool(np.array_equal(r_out.numpy(), rec) and np.array_equal(s_out.numpy(), st))
+    Te = (T // world) * world
+    per = Te // world
+    r_eq = torch.full((Te, P, rs), np.nan, dtype=torch.float64)
+    s_eq = torch.full((Te, P), -7, dtype=torch.int32)
+    D.gather_records_into(torch.from_numpy(rec[rank * per:(rank + 1) * per]),
+                          torch.from_numpy(st[rank * per:(rank + 1) * per]), r_eq, s_eq)
+    ok_into_eq = bool(np.array_equal(r_eq.numpy(), rec[:Te]) and np.array_equal(s_eq.numpy(), st[:Te]))
+    q.put((rank, ok_gather and ok_into and ok_into_eq, ok_pred, mx, counts))
     dist.destroy_process_group()
 
 
