@@ -24,6 +24,9 @@
 #ifndef FM_SELECT_STREAM_VPT
 #define FM_SELECT_STREAM_VPT 24   // values per thread above which fm_select streams the units
 #endif
+#ifndef FM_AB_SELECT_STREAM
+#define FM_AB_SELECT_STREAM 0     // timing builds only: the streaming kernel for every long unit
+#endif
 #ifndef FM_SELECT_STREAM_SB
 #define FM_SELECT_STREAM_SB 8     // loads per thread in flight in each streaming pass
 #endif
@@ -58,14 +61,12 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
     }
 }
 
-// Segments longer than the register budget (> 96 * 256 rows: a daily-frequency panel, a
-// huge cross-section): one workgroup per (segment, column) STREAMS the segment from HBM for
-// every pass instead of holding it in registers -- count / key range, the adaptive
+// Segments past the register budget (> 20,480 rows: a daily-frequency panel, a huge
+// cross-section; > 6,144 rows with a row mask or moments; the units the long-segment kernel
+// marked): one workgroup per (segment, column) STREAMS the segment from HBM for every pass instead of holding it in registers -- count / key range, the adaptive
 // histogram (hist_select: one histogram pass per level, one compaction pass), then the
 // moments if asked.  Exact order statistics, same lerps, same pivot as the register paths.
-__global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
-    __shared__ SelSmem sm;
-    const int s = blockIdx.x, c = blockIdx.y;
+__device__ __forceinline__ void stream_unit(const SelArgs& a, int s, int c, SelSmem& sm) {
     const int64_t r0 = a.seg_off[s];
     const int64_t L = a.seg_off[s + 1] - r0;
     const double* src = a.cols + (int64_t)c * a.col_stride + r0;
@@ -159,6 +160,211 @@ __global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
         a.hi[o] = hi;
         if (a.nvalid) a.nvalid[o] = n;
     }
+}
+
+// FB == false: one unit per workgroup (grid nseg x ncols).  FB == true: a fixed grid that
+// walks every unit and redoes those the long-segment kernel marked with nvalid == -1 (its
+// tail path could not finish them), lowest unit first, as select_kernel's fallback does.
+template <bool FB>
+__global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
+    __shared__ SelSmem sm;
+    if (!FB) {
+        stream_unit(a, blockIdx.x, blockIdx.y, sm);
+        return;
+    }
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
+    const int64_t per = (nunits + gridDim.x - 1) / gridDim.x;
+    const int64_t u0 = (int64_t)blockIdx.x * per, u1 = u0 + per < nunits ? u0 + per : nunits;
+    for (int64_t b = u0; b < u1; b += ST) {
+        const int64_t u = b + threadIdx.x;
+        bool mark = u < u1 && a.nvalid[u] == -1;
+        while (true) {
+            const uint64_t pick = block_min_u64<SNW>(mark ? (uint64_t)u : SENT, sm.u64s);
+            if (pick == SENT) break;   // block-uniform
+            if ((uint64_t)u == pick) mark = false;
+            __syncthreads();
+            stream_unit(a, (int)(pick % a.nseg), (int)(pick / a.nseg), sm);
+            __syncthreads();
+        }
+    }
+}
+
+// Long segments (6,145 .. 20,480 rows: C5's 20,000-firm months, a daily panel's short
+// windows): one 512-thread workgroup per (segment, column) holds the unit in registers
+// (VPT <= 40 values per thread, ONE coalesced HBM read of the unit).  Both winsorize tails:
+//   * per wave, the 64 thread minima (keys) sorted; T_w = the wave's q-th smallest,
+//     q = ceil((k+1)/8) for the largest needed rank k.  With c(T) = the number of valid
+//     thread minima <= T (ballots, every wave x every T_w), tau = the smallest T_w with
+//     c(tau) >= k+1: then k+1 threads own a value <= tau, so s[k] <= tau, and only the
+//     values < tau (a little more than k of them) can precede it;
+//   * those candidates are compacted to LDS (one block scan, both tails at once) and one
+//     wave per tail sorts them; a rank >= the candidate count is tau itself.
+// Units it cannot finish (ranks >= 512, > 512 candidates, too few valid thread minima) are
+// marked (nvalid = -1) and redone by the streaming kernel's fallback pass.  At <= 128 VGPRs
+// (4 waves per SIMD) two workgroups share a CU, so one unit's loads fly while the other
+// selects.
+constexpr int LT = 512;
+constexpr int LNW = LT / WAVE;
+constexpr int LONG_VPT = 40;
+constexpr int LCAP = 8 * WAVE;   // candidates per tail
+
+struct LongSmem {
+    uint64_t cand[2][LCAP];      // [lower / upper] candidate keys (upper: complemented)
+    uint64_t tw[2][LNW];         // per-wave thresholds T_w
+    int cnt[2][LNW][LNW];        // [tail][threshold][wave]: valid minima <= threshold
+    int ints[LNW];
+    uint64_t u64s[2 * LNW];
+};
+
+template <int VPT>
+__global__ __launch_bounds__(LT, 4) void select_long_kernel(SelArgs a) {
+    __shared__ LongSmem sm;
+    const int s = blockIdx.x, c = blockIdx.y;
+    const int tid = (int)threadIdx.x, lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
+    const int64_t r0 = a.seg_off[s];
+    const int L = (int)(a.seg_off[s + 1] - r0);
+    typedef const __attribute__((address_space(1))) char* gptr;
+    const gptr src = (gptr)(a.cols + (int64_t)c * a.col_stride + r0);
+    const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
+    uint32_t lb = (uint32_t)tid * 8u;
+    asm volatile("" : "+v"(lb));
+    double xv[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {   // unconditional (clamped) loads, masked after
+        const uint32_t off = lb + (uint32_t)(v * LT * 8);
+        const double x = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
+        xv[v] = off <= lastb && L > 0 ? x : NAN;
+    }
+    int cnt = 0;
+    double mn = NAN, mx = NAN;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        cnt += isnan(xv[v]) ? 0 : 1;
+        mn = hw_min(mn, xv[v]);
+        mx = hw_max(mx, xv[v]);
+    }
+    const int n = block_sum<LNW>(cnt, sm.ints);
+    const int64_t o = (int64_t)c * a.nseg + s;
+    double lo = NAN, hi = NAN;
+    if (n >= a.min_count && n > 0) {   // block-uniform
+        int i0, j0, i1, j1;
+        double g0, g1;
+        qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
+        qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
+        const int kl = j0, ku = n - 1 - i1;        // largest ranks needed from either end
+        const int ql = kl / LNW + 1, qu = ku / LNW + 1;
+        bool ok = ql <= WAVE && qu <= WAVE;
+        uint64_t tl = SENT, tu = SENT;
+        if (ok) {
+            uint64_t ka[1] = {isnan(mn) ? SENT : dkey(mn)};
+            uint64_t kb[1] = {isnan(mx) ? SENT : ~dkey(mx)};
+            wave_sort<1>(ka);
+            wave_sort<1>(kb);
+            if (lane == 0) {
+                sm.tw[0][w] = readlane_u64(ka[0], ql - 1);
+                sm.tw[1][w] = readlane_u64(kb[0], qu - 1);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < LNW; ++u) {
+                const uint64_t Ta = sm.tw[0][u], Tb = sm.tw[1][u];
+                const int ca = (int)__popcll(__ballot(ka[0] != SENT && ka[0] <= Ta));
+                const int cb = (int)__popcll(__ballot(kb[0] != SENT && kb[0] <= Tb));
+                if (lane == 0) {
+                    sm.cnt[0][u][w] = ca;
+                    sm.cnt[1][u][w] = cb;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < LNW; ++u) {
+                int ca = 0, cb = 0;
+#pragma unroll
+                for (int v = 0; v < LNW; ++v) {
+                    ca += sm.cnt[0][u][v];
+                    cb += sm.cnt[1][u][v];
+                }
+                const uint64_t Ta = sm.tw[0][u], Tb = sm.tw[1][u];
+                if (Ta != SENT && ca >= kl + 1 && Ta < tl) tl = Ta;
+                if (Tb != SENT && cb >= ku + 1 && Tb < tu) tu = Tb;
+            }
+            ok = tl != SENT && tu != SENT;
+        }
+        int clo = 0, chi = 0;
+        if (ok) {
+            const double tlo = kval(tl), thi = kval(~tu);
+            int cc = 0;
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) cc += (xv[v] < tlo ? 1 : 0) + (xv[v] > thi ? 0x10000 : 0);
+            int tot = 0;
+            const int off = block_excl_scan<LNW>(cc, sm.ints, &tot);
+            clo = tot & 0xFFFF;
+            chi = tot >> 16;
+            ok = clo <= LCAP && chi <= LCAP;
+            if (ok) {
+                int ol = off & 0xFFFF, oh = off >> 16;
+#pragma unroll
+                for (int v = 0; v < VPT; ++v) {
+                    double x = xv[v];
+                    asm volatile("" : "+v"(x));   // recompute (no SGPR masks kept from the count)
+                    if (x < tlo) sm.cand[0][ol++] = dkey(x);
+                    if (x > thi) sm.cand[1][oh++] = ~dkey(x);
+                }
+                __syncthreads();
+                if (w < 2) {
+                    uint64_t* buf = sm.cand[w];
+                    const int cn = w == 0 ? clo : chi;
+                    if (cn <= WAVE) wave_sort_lds<1>(buf, cn);
+                    else if (cn <= 2 * WAVE) wave_sort_lds<2>(buf, cn);
+                    else if (cn <= 4 * WAVE) wave_sort_lds<4>(buf, cn);
+                    else wave_sort_lds<8>(buf, cn);
+                }
+                __syncthreads();
+            }
+        }
+        if (!ok) {   // redone by select_stream_kernel<true>
+            if (tid == 0) a.nvalid[o] = -1;
+            return;
+        }
+        const int ci = n - 1 - j1, cj = ku;   // upper ranks in complemented order
+        const uint64_t k0 = i0 < clo ? sm.cand[0][i0] : tl;
+        const uint64_t k1 = j0 < clo ? sm.cand[0][j0] : tl;
+        const uint64_t k3 = ~(ci < chi ? sm.cand[1][ci] : tu);   // rank j1
+        const uint64_t k2 = ~(cj < chi ? sm.cand[1][cj] : tu);   // rank i1
+        lo = qlerp(kval(k0), kval(k1), g0, a.lerp_mode);
+        hi = qlerp(kval(k2), kval(k3), g1, a.lerp_mode);
+    }
+    if (a.center != nullptr) {
+        // Gram pivot: the midpoint of the cuts, else of the finite range, else 0
+        double cen = 0.5 * (lo + hi);
+        if (!isfinite(cen)) {   // block-uniform
+            const uint64_t m1 = block_min_u64<LNW>(isfinite(mn) ? dkey(mn) : SENT, sm.u64s);
+            const uint64_t m2 = block_min_u64<LNW>(isfinite(mx) ? ~dkey(mx) : SENT, sm.u64s + LNW);
+            cen = m1 == SENT || m2 == SENT ? 0.0 : 0.5 * (kval(m1) + kval(~m2));
+            if (!isfinite(cen)) cen = 0.0;
+        }
+        if (tid == 0) a.center[o] = cen;
+    }
+    if (tid == 0) {
+        a.lo[o] = lo;
+        a.hi[o] = hi;
+        a.nvalid[o] = n;
+    }
+}
+
+int launch_select_long(const SelArgs& a, int max_seg_len, hipStream_t st) {
+    const int vpt = (max_seg_len + LT - 1) / LT;
+    const dim3 grid(a.nseg, a.ncols);
+    if (vpt <= 16) hipLaunchKernelGGL(select_long_kernel<16>, grid, dim3(LT), 0, st, a);
+    else if (vpt <= 24) hipLaunchKernelGGL(select_long_kernel<24>, grid, dim3(LT), 0, st, a);
+    else if (vpt <= 32) hipLaunchKernelGGL(select_long_kernel<32>, grid, dim3(LT), 0, st, a);
+    else if (vpt <= LONG_VPT) hipLaunchKernelGGL(select_long_kernel<LONG_VPT>, grid, dim3(LT), 0, st, a);
+    else {
+        set_error("select long kernel: %d-row segments exceed %d", max_seg_len, LONG_VPT * LT);
+        return FM_ETOOBIG;
+    }
+    return FM_OK;
 }
 
 template <int VPT>
@@ -683,11 +889,21 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
               x.min_count, x.lerp_mode,  x.lo,    x.hi,     x.nvalid, x.mean, x.sd,  x.center};
     hipStream_t st = (hipStream_t)stream;
     const int vpt = (max_seg_len + ST - 1) / ST;
+    if (vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && row_mask == nullptr &&
+        x.mean == nullptr && nvalid != nullptr && !FM_AB_SELECT_STREAM) {
+        // past the 256-thread paths' register budget: the 512-thread register-resident
+        // kernel (one read per unit); the streaming kernel redoes the units it marked
+        const int rc = launch_select_long(a, max_seg_len, st);
+        if (rc != FM_OK) return rc;
+        FM_CHECK_LAUNCH("fm_select_cuts(long)");
+        hipLaunchKernelGGL(select_stream_kernel<true>, dim3(256), dim3(ST), 0, st, a);
+        FM_CHECK_LAUNCH("fm_select_cuts(long fallback)");
+        return FM_OK;
+    }
     if (vpt > FM_SELECT_STREAM_VPT) {
-        // past the wave paths' register budget: stream every unit from HBM / L2 (exact, any
-        // length).  Beyond 24 values per thread the register-resident workgroup kernel runs
-        // at 1-2 waves per SIMD (spilling at 96), the streaming one at 4.
-        hipLaunchKernelGGL(select_stream_kernel, dim3(nseg, ncols), dim3(ST), 0, st, a);
+        // longer still, or row masks / moments: stream every unit from HBM / L2 for each
+        // pass (exact, any length)
+        hipLaunchKernelGGL(select_stream_kernel<false>, dim3(nseg, ncols), dim3(ST), 0, st, a);
         FM_CHECK_LAUNCH("fm_select_cuts(stream)");
         return FM_OK;
     }

@@ -28,16 +28,19 @@ constexpr int CAND_CAP = 2048;
 constexpr int HB = 2048;     // hist_select: bins per level
 constexpr int HCAP = 256;    // hist_select: keys per candidate list (one wave sorts them)
 
-struct SelSmem {
+// Shared scratch of the workgroup select paths for NW-wave workgroups.
+template <int NW>
+struct SelSmemT {
     uint64_t buf[CAND_CAP];
     uint32_t hist[HB];
-    uint64_t u64s[2 * SNW];
-    double dbl[2 * SNW];
-    int ints[8];
+    uint64_t u64s[2 * NW];
+    double dbl[2 * NW];
+    int ints[NW > 8 ? NW : 8];
     uint64_t bc[4];
     int hs[4 * 3];           // hist_select: located (bin, count below, count in bin) per target
     uint32_t hcnt[4];        // hist_select: candidate list fill counters
 };
+using SelSmem = SelSmemT<SNW>;
 
 struct SelArgs {
     const double* cols;
@@ -501,10 +504,10 @@ __device__ __forceinline__ void hist_select_t(ForEach&& for_each, int nr, const 
     }
 }
 
-template <typename ForEach>
+template <int NW = SNW, typename ForEach>
 __device__ __forceinline__ void hist_select(ForEach&& for_each, int nr, const int* rk, uint64_t kmin,
-                                            uint64_t kmax, uint64_t* out, SelSmem& sm) {
-    hist_select_t<SNW, HB, HCAP>(for_each, nr, rk, kmin, kmax, out, sm);
+                                            uint64_t kmax, uint64_t* out, SelSmemT<NW>& sm) {
+    hist_select_t<NW, HB, HCAP>(for_each, nr, rk, kmin, kmax, out, sm);
 }
 
 // Number of entries of the ascending list L[0..64) that precede v in the merged order:
@@ -530,19 +533,23 @@ __device__ __forceinline__ int merge_count(const uint64_t* L, uint64_t v, bool i
 //   lj+1 threads own a value <= tau_lo, so s[lj] <= tau_lo, and only the values < tau_lo
 //   (a few more than lj) can precede it: they are compacted with one packed scan and
 //   sorted by one wave.  The upper tail is the same on complemented keys of the maxima.
-template <int VPT>
+template <int VPT, int NW = SNW>
 __device__ __forceinline__ bool select_tails(const double (&xv)[VPT], double mn, double mx, int n,
                                              int li, int lj, int hi_i, int hi_j, uint64_t& k0,
-                                             uint64_t& k1, uint64_t& k2, uint64_t& k3, SelSmem& sm) {
+                                             uint64_t& k1, uint64_t& k2, uint64_t& k3, SelSmemT<NW>& sm) {
+    constexpr int NT = NW * WAVE;
+    // candidate list capacity per tail (4 * 64 keys; 8 * 64 for the 8-wave long-month path)
+    constexpr int CC = NW >= 8 ? 8 * WAVE : 4 * WAVE;
+    static_assert(2 * NT + 2 * (CAND_CAP / 4) <= CAND_CAP && CC <= CAND_CAP / 4, "select_tails: LDS layout");
     const int ci = n - 1 - hi_j, cj = n - 1 - hi_i;   // upper-tail ranks in complemented order
-    if (lj >= ST || cj >= ST) return false;
+    if (lj >= NT || cj >= NT) return false;
     uint64_t a[1] = {isnan(mn) ? SENT : dkey(mn)};
     uint64_t b[1] = {isnan(mx) ? SENT : ~dkey(mx)};
     wave_sort<1>(a);
     wave_sort<1>(b);
     const int w = threadIdx.x / WAVE, lane = lane_id();
-    uint64_t* Llo = sm.buf + CAND_CAP - 8 * WAVE;       // [4][64] sorted thread minima
-    uint64_t* Lhi = sm.buf + CAND_CAP - 4 * WAVE;       // [4][64] sorted complemented maxima
+    uint64_t* Llo = sm.buf + CAND_CAP - 2 * NT;         // [NW][64] sorted thread minima
+    uint64_t* Lhi = sm.buf + CAND_CAP - NT;             // [NW][64] sorted complemented maxima
     __syncthreads();   // sm.buf may still be read by a previous phase
     Llo[w * WAVE + lane] = a[0];
     Lhi[w * WAVE + lane] = b[0];
@@ -552,14 +559,14 @@ __device__ __forceinline__ bool select_tails(const double (&xv)[VPT], double mn,
     if (lane <= lj && a[0] != SENT) {
         int r = lane;
 #pragma unroll
-        for (int u = 0; u < SNW; ++u)
+        for (int u = 0; u < NW; ++u)
             if (u != w) r += merge_count(Llo + u * WAVE, a[0], u < w);
         if (r == lj) sm.bc[0] = a[0];
     }
     if (lane <= cj && b[0] != SENT) {
         int r = lane;
 #pragma unroll
-        for (int u = 0; u < SNW; ++u)
+        for (int u = 0; u < NW; ++u)
             if (u != w) r += merge_count(Lhi + u * WAVE, b[0], u < w);
         if (r == cj) sm.bc[1] = b[0];
     }
@@ -571,27 +578,32 @@ __device__ __forceinline__ bool select_tails(const double (&xv)[VPT], double mn,
 #pragma unroll
     for (int v = 0; v < VPT; ++v) cnt += (xv[v] < tlo ? 1 : 0) + (xv[v] > thi ? 0x10000 : 0);
     int tot = 0;
-    const int off = block_excl_scan<SNW>(cnt, sm.ints, &tot);
+    const int off = block_excl_scan<NW>(cnt, sm.ints, &tot);
     const int clo = tot & 0xFFFF, chi = tot >> 16;
     constexpr int HALF = CAND_CAP / 4;
-    if (clo > 4 * WAVE || chi > 4 * WAVE) return false;   // block-uniform
+    if (clo > CC || chi > CC) return false;   // block-uniform
     {
         int ol = off & 0xFFFF, oh = HALF + (off >> 16);
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-            if (xv[v] < tlo) sm.buf[ol++] = dkey(xv[v]);
-            if (xv[v] > thi) sm.buf[oh++] = ~dkey(xv[v]);
+            // recompute the compares (the counting pass's would stay live as SGPR masks)
+            double x = xv[v];
+            asm volatile("" : "+v"(x));
+            if (x < tlo) sm.buf[ol++] = dkey(x);
+            if (x > thi) sm.buf[oh++] = ~dkey(x);
         }
         __syncthreads();
     }
     if (w == 0) {
         if (clo <= WAVE) wave_sort_lds<1>(sm.buf, clo);
         else if (clo <= 2 * WAVE) wave_sort_lds<2>(sm.buf, clo);
-        else wave_sort_lds<4>(sm.buf, clo);
+        else if (CC <= 4 * WAVE || clo <= 4 * WAVE) wave_sort_lds<4>(sm.buf, clo);
+        else wave_sort_lds<(CC > 4 * WAVE ? 8 : 4)>(sm.buf, clo);
     } else if (w == 1) {
         if (chi <= WAVE) wave_sort_lds<1>(sm.buf + HALF, chi);
         else if (chi <= 2 * WAVE) wave_sort_lds<2>(sm.buf + HALF, chi);
-        else wave_sort_lds<4>(sm.buf + HALF, chi);
+        else if (CC <= 4 * WAVE || chi <= 4 * WAVE) wave_sort_lds<4>(sm.buf + HALF, chi);
+        else wave_sort_lds<(CC > 4 * WAVE ? 8 : 4)>(sm.buf + HALF, chi);
     }
     __syncthreads();
     k0 = li < clo ? sm.buf[li] : tlo_k;
@@ -634,24 +646,37 @@ __device__ __forceinline__ double qlerp(double a, double b, double g, int mode) 
 
 // One (segment, column) unit on a 256-thread workgroup: the general path (any ranks, row
 // masks, up to 96 * 256 rows).  Block-uniform control flow.
-template <int VPT>
-__device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, SelSmem& sm) {
+template <int VPT, int NW = SNW, bool MARK = false>
+__device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, SelSmemT<NW>& sm) {
+    constexpr int NT = NW * WAVE;
     const int64_t r0 = a.seg_off[s];
     const int L = (int)(a.seg_off[s + 1] - r0);
     const double* src = a.cols + (int64_t)c * a.col_stride + r0;
     // Unconditional loads (index clamped, masked after): a load under a runtime condition
     // makes hipcc wait vmcnt(0) per load and serializes the HBM round trips.
-    const int last = L > 0 ? L - 1 : 0;
-    const uint8_t* mbase = a.mask ? a.mask + r0 : (const uint8_t*)src;
-    const int mand = a.mask ? 0xFF : 0, mor = a.mask ? 0 : 1;
+    // Wave-uniform base (SGPRs) + the lane's 32-bit byte offset: no 64-bit address per load.
+    typedef const __attribute__((address_space(1))) char* gptr;
+    const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
+    uint32_t lb = (uint32_t)threadIdx.x * 8u;
+    asm volatile("" : "+v"(lb));
     double xv[VPT];
+    if (a.mask == nullptr) {   // block-uniform
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-        const int idx = threadIdx.x + v * ST;
-        const int ci = idx < L ? idx : last;
-        const double x = src[ci];
-        const int m = (mbase[ci] & mand) | mor;
-        xv[v] = (idx < L && m != 0) ? x : NAN;
+        for (int v = 0; v < VPT; ++v) {
+            const uint32_t off = lb + (uint32_t)(v * NT * 8);
+            const double x = *(const __attribute__((address_space(1))) double*)((gptr)src + (off < lastb ? off : lastb));
+            xv[v] = off <= lastb && L > 0 ? x : NAN;
+        }
+    } else {
+        const gptr mb = (gptr)(a.mask + r0);
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            const uint32_t off = lb + (uint32_t)(v * NT * 8);
+            const uint32_t oc = off < lastb ? off : lastb;
+            const double x = *(const __attribute__((address_space(1))) double*)((gptr)src + oc);
+            const uint8_t m = *(mb + (oc >> 3));
+            xv[v] = (off <= lastb && L > 0 && m != 0) ? x : NAN;
+        }
     }
     // thread count / min / max (NaN-ignoring hardware min / max)
     int cnt = 0;
@@ -662,7 +687,7 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
         mn = hw_min(mn, xv[v]);
         mx = hw_max(mx, xv[v]);
     }
-    const int n = block_sum<SNW>(cnt, sm.ints);
+    const int n = block_sum<NW>(cnt, sm.ints);
     double lo = NAN, hi = NAN;
     const bool apply = n >= a.min_count && n > 0;
     if (apply) {
@@ -671,7 +696,13 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
         qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
         qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
         uint64_t k0, k1, k2, k3;
-        if (!select_tails<VPT>(xv, mn, mx, n, i0, j0, i1, j1, k0, k1, k2, k3, sm)) {
+        const bool fast = select_tails<VPT, NW>(xv, mn, mx, n, i0, j0, i1, j1, k0, k1, k2, k3, sm);
+        if (MARK && !fast) {
+            // MARK: the rare unit the tail path cannot finish is redone by a fallback pass
+            if (threadIdx.x == 0) a.nvalid[(int64_t)c * a.nseg + s] = -1;
+            return;
+        }
+        if (!MARK && !fast) {
             // any ranks (pandas middle quantiles, overflowing tails): adaptive histogram
             uint64_t kmn = SENT, kmx = 0;
 #pragma unroll
@@ -681,11 +712,11 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
                     kmn = k < kmn ? k : kmn;
                     kmx = k > kmx ? k : kmx;
                 }
-            kmn = block_min_u64<SNW>(kmn, sm.u64s);
-            kmx = block_max_u64<SNW>(kmx, sm.u64s + SNW);
+            kmn = block_min_u64<NW>(kmn, sm.u64s);
+            kmx = block_max_u64<NW>(kmx, sm.u64s + NW);
             const int rk[4] = {i0, j0, i1, j1};
             uint64_t ko[4];
-            hist_select([&](auto&& f) {
+            hist_select<NW>([&](auto&& f) {
 #pragma unroll
                 for (int v = 0; v < VPT; ++v) f(xv[v]);
             }, 4, rk, kmn, kmx, ko, sm);
@@ -699,14 +730,14 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
         // uniform branch: lo / hi are block-uniform)
         double cen = 0.5 * (lo + hi);
         if (!isfinite(cen)) {
-            const double m1 = block_min_f64<SNW>(isfinite(mn) ? mn : NAN, sm.dbl);
-            const double m2 = -block_min_f64<SNW>(isfinite(mx) ? -mx : NAN, sm.dbl);
+            const double m1 = block_min_f64<NW>(isfinite(mn) ? mn : NAN, sm.dbl);
+            const double m2 = -block_min_f64<NW>(isfinite(mx) ? -mx : NAN, sm.dbl);
             cen = 0.5 * (m1 + m2);
             if (!isfinite(cen)) cen = 0.0;
         }
         if (threadIdx.x == 0) a.center[(int64_t)c * a.nseg + s] = cen;
     }
-    if (a.mean != nullptr) {
+    if (!MARK && a.mean != nullptr) {   // (MARK callers route moment requests elsewhere)
         // Moments of the clipped values (pandas clip ignores NaN bounds).  One pass about a
         // pivot p inside the data (a finite cut, else the smallest finite value):
         // mean = p + S1/n, var = (S2 - S1^2/n)/(n-1).
@@ -714,7 +745,7 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
         if (!isfinite(lo) && !isfinite(hi)) {
             // no cuts (short month): pivot = the smallest finite value
             double m2 = isfinite(mn) ? mn : NAN;
-            p = block_min_f64<SNW>(m2, sm.dbl);
+            p = block_min_f64<NW>(m2, sm.dbl);
             if (!isfinite(p)) p = 0.0;
         }
         double s1 = 0.0, s2 = 0.0;
@@ -727,7 +758,7 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
             s1 += d;
             s2 = fma(d, d, s2);
         }
-        double2 r = block_sum2<SNW>(s1, s2, sm.dbl);
+        double2 r = block_sum2<NW>(s1, s2, sm.dbl);
         if (threadIdx.x == 0) {
             const double mu = n > 0 ? p + r.x / (double)n : NAN;
             a.mean[(int64_t)c * a.nseg + s] = mu;

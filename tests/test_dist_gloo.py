@@ -87,3 +87,55 @@ def test_sharded_records_equal_single_process(world):
         assert ok_gather and ok_pred, rank
         assert mx == float(world)
         assert sum(counts) == 37
+
+
+FIXTURE = os.path.join(ROOT, "tests", "golden", "shard_pred.npz")
+
+
+def _pred_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "fm-returnprediction_amd"))
+    from fmcore import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = np.load(FIXTURE)
+    # world 2: rank 0 holds shards 0 and 1 (their rows are disjoint), rank 1 shard 2
+    mine = [0, 1] if (world == 2 and rank == 0) else [2] if world == 2 else [rank]
+    pred = sum(g[f"pred{i}"] for i in mine)
+    pst = sum(g[f"pst{i}"] for i in mine)
+    tp, ts = D.combine_predictive(torch.from_numpy(pred.copy()), torch.from_numpy(pst.copy()))
+    tp, ts = tp.numpy(), ts.numpy()
+    keep = (g["full_pst"] & 1) != 0
+    same_st = bool(np.array_equal(ts, g["full_pst"]))
+    a, b = tp[keep], g["full_pred"][keep]
+    same_pred = bool(np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(a[~np.isnan(a)], b[~np.isnan(b)]))
+    q.put((rank, same_st, same_pred))
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not os.path.exists(FIXTURE), reason="tools/dump_shard_pred.py fixture not generated")
+@pytest.mark.parametrize("world", [2, 3])
+def test_combine_predictive_real_shard_outputs(world):
+    """combine_predictive on the real device pipeline's per-shard predictive records
+    (tests/golden/shard_pred.npz, written by tools/dump_shard_pred.py on the GPU: a ragged
+    96-month panel in 3 shard_bounds ranges, each shard's time-series stage with its own
+    moments).  The SUM all-reduce relies on every row of another shard's months being
+    exactly 0 (records and status); the combined result must equal the unsharded run bit for
+    bit on every fitted row, and the status words exactly."""
+    g = np.load(FIXTURE)
+    for i in range(3):   # the fixture's premise: the shards' fitted rows are disjoint
+        for j in range(i + 1, 3):
+            assert not ((g[f"pst{i}"] & 1) & (g[f"pst{j}"] & 1)).any()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pred_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, same_st, same_pred in out:
+        assert same_st and same_pred, rank

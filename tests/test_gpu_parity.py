@@ -177,6 +177,49 @@ def test_long_segment_cuts_bit_exact(E, n):
         assert _same([lo[t]], [O.pandas_quantile(y, 0.2)]) and _same([hi[t]], [O.pandas_quantile(y, 0.5)])
 
 
+def _thread_clustered_segment(rng, n):
+    """Both tails sit in the rows of 64 of the long kernel's 512 threads (row % 512), so the
+    thread-extremum bound leaves far more than 512 candidates: the unit is marked and the
+    streaming fallback redoes it."""
+    x = rng.standard_normal(n)
+    r = np.arange(n) % 512
+    x[r < 64] -= 100.0
+    x[r >= 448] += 100.0
+    return x
+
+
+@pytest.mark.parametrize("maxlen", [8192, 12288, 16384, 20480])
+def test_long_month_register_select_bit_exact(E, maxlen):
+    """Months of 6,145 .. 20,480 rows (C5's 20,000-firm cross-sections) take the 512-thread
+    register-resident kernel (one read per unit; VPT 16 / 24 / 32 / 40 by the longest month)
+    and the streaming fallback for the units it marks: bit-exact against np.percentile on
+    the adversarial kinds, the hard segments and thread-clustered tails, next to short
+    segments (which ride the same launch)."""
+    rng = np.random.default_rng(maxlen)
+    lengths = sorted({1, 5, 257, 5000, 6145, maxlen - 1, maxlen, (6145 + maxlen) // 2})
+    segs = _adversarial_segments(rng, lengths)
+    segs += [_hard_segment(rng, maxlen, k) for k in ("t2", "ties", "const", "cluster")]
+    segs += [_thread_clustered_segment(rng, maxlen), _thread_clustered_segment(rng, 6200)]
+    vals = np.concatenate(segs)
+    labels = np.repeat(np.arange(len(segs)), [len(s) for s in segs])
+    panel = E.panel_from_arrays([vals], ["v"], labels)
+    assert panel.max_seg_len == maxlen
+    for qa, qb in ((1, 99), (0, 100), (5, 95), (25, 75)):
+        cuts = E.select_cuts(panel, qa / 100, qb / 100, 1, E.LERP_NUMPY)
+        lo, hi = cuts.lo.cpu().numpy()[0], cuts.hi.cpu().numpy()[0]
+        nv = cuts.nvalid.cpu().numpy()[0]
+        assert (nv >= 0).all()    # every marked unit was redone
+        for t, s in enumerate(segs):
+            v = s[~np.isnan(s)]
+            assert nv[t] == len(v)
+            if len(v) == 0:
+                assert np.isnan(lo[t]) and np.isnan(hi[t])
+                continue
+            with np.errstate(invalid="ignore"):
+                ra, rb = np.percentile(v, qa), np.percentile(v, qb)
+            assert _same([lo[t]], [ra]) and _same([hi[t]], [rb]), (qa, qb, t, len(v), lo[t], ra, hi[t], rb)
+
+
 def test_masked_middle_quantiles_hist_select(E):
     """NYSE-style row-masked middle quantiles (pandas lerp) through the workgroup path's
     adaptive histogram select, incl. clustered keys that need the refinement levels."""
@@ -735,44 +778,132 @@ def test_pipeline_c5_rank_shard_full_size(E):
     (2) the FM summaries (mean, NW t) and the 120/60 rolling means against the oracle's
     restatement applied to the device's own monthly records (12,500-long series)."""
     import torch
-    from fmcore import lewellen as LW, synth
+    from fmcore import lewellen as LW
     T, N, seed, m0 = 12500, 20000, 20150101, 50000
     panel = E.panel_synthetic(T, N, seed, month0=m0)
     cfg = LW.PipelineConfig()
     assert not E.ts_fused_fits(T, 16, cfg.window, cfg.lag, predictive=True)
     out = LW.run_pipeline(panel, cfg)
     torch.cuda.synchronize()
-    res = out.res
+    _check_records_vs_oracle(out.res, out.model_names, (0, 1, T // 2, T - 1), N, seed, m0)
+    assert ((out.res.status.cpu().numpy() & 1) != 0).all()
+    _check_series_vs_restatement(out.res, out.summary, out.rolling, cols=2)
+
+
+def _check_records_vs_oracle(res, names, months, N, seed, m0=0):
+    """Sampled months' monthly records (every problem) against the oracle run on exactly
+    those months (host regeneration of the same counter-hash rows)."""
+    from fmcore import lewellen as LW, synth
     rec = res.rec.cpu().numpy()
     st = res.status.cpu().numpy()
     models = {name: ("retx", xs, (0, 1, 2)) for name, xs in LW.table2_models().items()}
     models["Figure 1"] = ("retx", LW.FIG1_VARS, (0, 2))
-    for t in (0, 1, T // 2, T - 1):
+    for t in months:
         a = synth.synth_arrays(1, N, seed, month0=m0 + t)
         cols = {c: a[c] for c in synth.WINSOR_VARS}
         ref = O.pipeline_arrays(cols, np.array([0, N], dtype=np.int64), a["me"], a["nyse"].astype(bool),
                                 models, None)
         for k, p in enumerate(res.problems):
-            r = ref[(out.model_names[p.model], p.level)]
+            r = ref[(names[p.model], p.level)]
             assert (st[t, k] & 1) != 0 and list(r["month"]) == [0], (t, k)
             assert int(rec[t, k, res.pmax + 1]) == int(r["N"][0])
             b = r["params"][0]
             a_ = rec[t, k, :p.K + 1]
             assert np.all(np.abs(a_ - b) <= RTOL * np.maximum(np.abs(b), np.sqrt(np.mean(b ** 2)))), (t, k)
             assert abs(rec[t, k, res.pmax] - r["R2"][0]) <= RTOL * abs(r["R2"][0])
-    mean = out.summary.mean.cpu().numpy()
-    tstat = out.summary.tstat.cpu().numpy()
-    roll = out.rolling.cpu().numpy()
+
+
+def _rolling_rows(x, rows, window=120, min_periods=60):
+    """oracle.rolling_mean's definition evaluated at the given rows only (long series)."""
+    out = np.full(len(rows), np.nan)
+    for i, r in enumerate(rows):
+        w = x[max(0, r - window + 1):r + 1]
+        w = w[np.isfinite(w)]
+        if w.size >= min_periods:
+            out[i] = w.sum() / w.size
+    return out
+
+
+def _check_series_vs_restatement(res, summ, roll, cols=2, pred=None, pst=None, psumm=None):
+    """FM means, NW(4) t-stats and 120/60 rolling means of the device's own monthly records
+    against the oracle's restatement (oracle.newey_west_mean_se / rolling_mean); the
+    predictive-slope FM summary likewise from the device's predictive records."""
+    rec = res.rec.cpu().numpy()
+    st = res.status.cpu().numpy()
+    mean, tstat, rl = summ.mean.cpu().numpy(), summ.tstat.cpu().numpy(), roll.cpu().numpy()
     for k, p in enumerate(res.problems):
         fit = np.nonzero(st[:, k] & 1)[0]
-        assert fit.size == T
         for j in range(1, p.K + 1):
             x = rec[fit, k, j]
             m = x.mean()
             assert scalar_close(mean[k, j], m, RTOL, 1e-12), (k, j)
             assert scalar_close(tstat[k, j], m / O.newey_west_mean_se(x, 4), RTOL, 1e-12), (k, j)
-        for j in range(2):   # intercept and first slope (the restatement loops per row)
-            assert_series_close(roll[k, :T, j], O.rolling_mean(rec[fit, k, j], 120, 60), f"roll {k}/{j}")
+        rows = np.unique(np.concatenate([np.arange(min(fit.size, 300)),
+                                         np.linspace(0, fit.size - 1, 700).astype(np.int64)]))
+        for j in range(cols):
+            assert_series_close(rl[k, rows, j], _rolling_rows(rec[fit, k, j], rows), f"roll {k}/{j}")
+    if pred is not None:
+        pr, ps = pred.cpu().numpy(), pst.cpu().numpy()
+        pm, pt = psumm.mean.cpu().numpy(), psumm.tstat.cpu().numpy()
+        for k in range(len(res.problems)):
+            x = pr[k, (ps[k] & 1) != 0, 0]
+            assert x.size > 0
+            assert scalar_close(pm[k, 0], x.mean(), RTOL, 1e-12), k
+            assert scalar_close(pt[k, 0], x.mean() / O.newey_west_mean_se(x, 4), RTOL, 1e-12), k
+
+
+def test_pipeline_headline_panel_full_size(E):
+    """The bench's own panel (600 months x 5,000 firms x 15 characteristics, seed 1, generated
+    in HBM by fm_gen_panel) through the bench's step (ShardedStep, world size 1): six sampled
+    months' records for all 11 problems against the oracle on those months; FM summaries,
+    rolling means and the predictive-slope summary against the oracle's restatement applied
+    to the device's records."""
+    import torch
+    from fmcore import lewellen as LW
+    from fmcore.step import ShardedStep
+    T, N, seed = 600, 5000, 1
+    panel = E.panel_synthetic(T, N, seed)
+    step = ShardedStep(panel, LW.PipelineConfig(), LW.table2_models())
+    gres, summ, psumm = step.eager()
+    torch.cuda.synchronize()
+    names = list(LW.table2_models()) + ["Figure 1"]
+    _check_records_vs_oracle(gres, names, (0, 1, 150, 299, 451, T - 1), N, seed)
+    ix, summ2, roll, pred, pst = LW.time_series_stage(gres, LW.PipelineConfig())
+    assert _same(summ2.mean.cpu().numpy(), summ.mean.cpu().numpy())
+    _check_series_vs_restatement(gres, summ, roll, cols=3, pred=pred, pst=pst, psumm=psumm)
+
+
+def test_time_series_stage_gathered_c5_length(E):
+    """C5's time-series stage at gathered length: every rank runs it on the full 100,000-month
+    series of 11 problems (reference src/regressions.py:78-131, calc_Lewellen_2014.py:926).
+    The series = a 12,500-month local pass's records tiled 8 times (what the all-gather of 8
+    ranks' records assembles); the predictive slopes for the rank-4 month range use that
+    pass's own moments.  Checked: summaries, NW t-stats, rolling means (intercept + first
+    slope) and the predictive-slope summary against the oracle's restatement."""
+    import torch
+    from fmcore import lewellen as LW
+    Tl, world, rank = 12500, 8, 4
+    panel = E.panel_synthetic(Tl, 200, 77, month0=rank * Tl)
+    cfg = LW.PipelineConfig()
+    res, _, _, _, _ = LW.local_stage(panel, cfg, LW.table2_models())
+    rec = res.rec.repeat(world, 1, 1).contiguous()
+    st = res.status.repeat(world, 1).contiguous()
+    st[3, :] = 0                       # a few unfitted months in the gathered series
+    rec[3, :, :] = float("nan")
+    g = E.FMResult(problems=res.problems, rec=rec, status=st, pmax=res.pmax, moments=res.moments,
+                   mom_stride=res.mom_stride)
+    assert not E.ts_fused_fits(rec.shape[0], res.pmax, cfg.window, cfg.lag, predictive=True)
+    ix, summ, roll, pred, pst = LW.time_series_stage(g, cfg, moments=res.moments, seg_lo=rank * Tl,
+                                                     seg_hi=(rank + 1) * Tl)
+    psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
+    torch.cuda.synchronize()
+    assert np.array_equal(ix.count.cpu().numpy(), (st.cpu().numpy() & 1).sum(axis=0))
+    _check_series_vs_restatement(g, summ, roll, cols=2, pred=pred, pst=pst, psumm=psumm)
+    # predictive rows exist only for the rank's own months (index = fitted-month position)
+    ps = pst.cpu().numpy()
+    for k in range(len(res.problems)):
+        rows = np.nonzero(ps[k] & 1)[0]
+        assert rows.min() >= rank * Tl - 1 and rows.max() < (rank + 1) * Tl, k
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
