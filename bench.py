@@ -126,6 +126,7 @@ def main():
     ms_step = dt / args.steps * 1e3
     whole = rows_local * b_row / (ms_step * 1e-3) / 1e9
 
+    stream = _stream_copy_gbs(dev)
     result = {
         "metric": METRIC,
         "value": rows_local * world * args.steps / dt,
@@ -153,6 +154,7 @@ def main():
                      "traffic_ratio": traffic["bytes"] / cand[dom] if traffic else None,
                      "traffic_source": traffic["source"] if traffic else None,
                      "bytes_per_launch": cand[dom], "avg_launch_ms": dom_ms,
+                     "measured_copy_peak": stream, "frac_of_measured_copy": achieved / stream,
                      "whole_pass": {"bytes_per_row": b_row, "achieved": whole, "frac": whole / HBM_PEAK_GBS,
                                     "ms_per_step": ms_step}},
         "kernel_ms": {k: round(v, 4) for k, v in dev_ms.items()},
@@ -220,6 +222,25 @@ def c5_shard_stage(args, E, LW, reps=3):
             "whole_pass_frac": rows * (15 * 8 + 8 + 1) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "note": "eager launches; rank 4 of the 8-GPU C5 split (local pass + time series on the "
                     "100,000-month gathered series; the all-gather is not timed)"}
+
+
+def _stream_copy_gbs(dev, nbytes=1 << 30, reps=10):
+    """The achievable HBM rate on this box: a 1 GiB device-to-device copy (read + write
+    bytes) timed with HIP events -- reported beside the 8 TB/s spec peak."""
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def _lib_sha():
@@ -341,6 +362,8 @@ def cpu_baseline(panel, args, LW):
         out["ref_over_port"] = d["ref_over_port"]
         out["reference_value_est"] = out["value"] * d["ref_over_port"]
         out["ref_over_port_sample"] = d["sample"] + f", python {d['interpreter']}, profiles/ref_vs_port.json"
+        out["ref_over_port_host"] = ("the 8-core build container (the reference cannot travel to the GPU box); "
+                                     "reference_value_est = this host's port rate x that ratio")
     return out
 
 

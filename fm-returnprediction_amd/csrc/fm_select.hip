@@ -24,6 +24,15 @@
 #ifndef FM_SELECT_STREAM_VPT
 #define FM_SELECT_STREAM_VPT 24   // values per thread above which fm_select streams the units
 #endif
+#ifndef FM_AB_LONG
+#define FM_AB_LONG 0              // timing builds only: 1 loads + count, 2 no candidate sort
+#endif
+#ifndef FM_LONG_PERSIST
+#define FM_LONG_PERSIST 0         // 1: persistent grid, next unit prefetched (timing builds: slower)
+#endif
+#ifndef FM_LONG_PER_CU
+#define FM_LONG_PER_CU 1
+#endif
 #ifndef FM_AB_SELECT_STREAM
 #define FM_AB_SELECT_STREAM 0     // timing builds only: the streaming kernel for every long unit
 #endif
@@ -216,103 +225,140 @@ struct LongSmem {
     uint64_t u64s[2 * LNW];
 };
 
-template <int VPT>
-__global__ __launch_bounds__(LT, 4) void select_long_kernel(SelArgs a) {
+// PERSIST: one workgroup per CU (<= 256 VGPRs: the prefetched unit and the candidate sort
+// live together without spills) walks the units; the next unit's loads are issued as soon
+// as this unit's candidates sit in LDS, so they fly during the candidate sorts.
+template <int VPT, bool PERSIST>
+__global__ __launch_bounds__(LT, PERSIST ? 2 : 4) void select_long_kernel(SelArgs a) {
     __shared__ LongSmem sm;
-    const int s = blockIdx.x, c = blockIdx.y;
     const int tid = (int)threadIdx.x, lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
-    const int64_t r0 = a.seg_off[s];
-    const int L = (int)(a.seg_off[s + 1] - r0);
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
+    int64_t u = PERSIST ? (int64_t)blockIdx.x : (int64_t)blockIdx.y * a.nseg + blockIdx.x;
+    if (u >= nunits) return;   // block-uniform
     typedef const __attribute__((address_space(1))) char* gptr;
-    const gptr src = (gptr)(a.cols + (int64_t)c * a.col_stride + r0);
-    const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
     uint32_t lb = (uint32_t)tid * 8u;
     asm volatile("" : "+v"(lb));
     double xv[VPT];
+    auto load = [&](int64_t uu) -> int {   // unconditional (clamped) loads, masked at use
+        const int s = (int)(uu % a.nseg), c = (int)(uu / a.nseg);
+        const int64_t r0 = a.seg_off[s];
+        const int L = (int)(a.seg_off[s + 1] - r0);
+        const gptr src = (gptr)(a.cols + (int64_t)c * a.col_stride + r0);
+        const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {   // unconditional (clamped) loads, masked after
-        const uint32_t off = lb + (uint32_t)(v * LT * 8);
-        const double x = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
-        xv[v] = off <= lastb && L > 0 ? x : NAN;
-    }
-    int cnt = 0;
-    double mn = NAN, mx = NAN;
-#pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-        cnt += isnan(xv[v]) ? 0 : 1;
-        mn = hw_min(mn, xv[v]);
-        mx = hw_max(mx, xv[v]);
-    }
-    const int n = block_sum<LNW>(cnt, sm.ints);
-    const int64_t o = (int64_t)c * a.nseg + s;
-    double lo = NAN, hi = NAN;
-    if (n >= a.min_count && n > 0) {   // block-uniform
-        int i0, j0, i1, j1;
-        double g0, g1;
-        qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
-        qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
-        const int kl = j0, ku = n - 1 - i1;        // largest ranks needed from either end
-        const int ql = kl / LNW + 1, qu = ku / LNW + 1;
-        bool ok = ql <= WAVE && qu <= WAVE;
-        uint64_t tl = SENT, tu = SENT;
-        if (ok) {
-            uint64_t ka[1] = {isnan(mn) ? SENT : dkey(mn)};
-            uint64_t kb[1] = {isnan(mx) ? SENT : ~dkey(mx)};
-            wave_sort<1>(ka);
-            wave_sort<1>(kb);
-            if (lane == 0) {
-                sm.tw[0][w] = readlane_u64(ka[0], ql - 1);
-                sm.tw[1][w] = readlane_u64(kb[0], qu - 1);
-            }
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < LNW; ++u) {
-                const uint64_t Ta = sm.tw[0][u], Tb = sm.tw[1][u];
-                const int ca = (int)__popcll(__ballot(ka[0] != SENT && ka[0] <= Ta));
-                const int cb = (int)__popcll(__ballot(kb[0] != SENT && kb[0] <= Tb));
-                if (lane == 0) {
-                    sm.cnt[0][u][w] = ca;
-                    sm.cnt[1][u][w] = cb;
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < LNW; ++u) {
-                int ca = 0, cb = 0;
-#pragma unroll
-                for (int v = 0; v < LNW; ++v) {
-                    ca += sm.cnt[0][u][v];
-                    cb += sm.cnt[1][u][v];
-                }
-                const uint64_t Ta = sm.tw[0][u], Tb = sm.tw[1][u];
-                if (Ta != SENT && ca >= kl + 1 && Ta < tl) tl = Ta;
-                if (Tb != SENT && cb >= ku + 1 && Tb < tu) tu = Tb;
-            }
-            ok = tl != SENT && tu != SENT;
+        for (int v = 0; v < VPT; ++v) {
+            const uint32_t off = lb + (uint32_t)(v * LT * 8);
+            xv[v] = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
         }
-        int clo = 0, chi = 0;
-        if (ok) {
-            const double tlo = kval(tl), thi = kval(~tu);
-            int cc = 0;
+        return L;
+    };
+    int L = load(u);
+    while (true) {
+        const int64_t un = u + gridDim.x;
+        const bool more = PERSIST && un < nunits;   // block-uniform
+        int Ln = 0;
+        bool fetched = false;
+        const int s = (int)(u % a.nseg), c = (int)(u / a.nseg);
+        const int64_t o = (int64_t)c * a.nseg + s;
+        {
+            const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
 #pragma unroll
-            for (int v = 0; v < VPT; ++v) cc += (xv[v] < tlo ? 1 : 0) + (xv[v] > thi ? 0x10000 : 0);
-            int tot = 0;
-            const int off = block_excl_scan<LNW>(cc, sm.ints, &tot);
-            clo = tot & 0xFFFF;
-            chi = tot >> 16;
-            ok = clo <= LCAP && chi <= LCAP;
+            for (int v = 0; v < VPT; ++v)
+                if (!(lb + (uint32_t)(v * LT * 8) <= lastb && L > 0)) xv[v] = NAN;
+        }
+        int cnt = 0;
+        double mn = NAN, mx = NAN;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            cnt += isnan(xv[v]) ? 0 : 1;
+            mn = hw_min(mn, xv[v]);
+            mx = hw_max(mx, xv[v]);
+        }
+        const int n = block_sum<LNW>(cnt, sm.ints);
+        double lo = NAN, hi = NAN;
+        bool ok = true;
+        if (FM_AB_LONG == 1) {   // timing builds only: the load + count floor
+            if (more) Ln = load(un);
+            if (tid == 0) a.nvalid[o] = n, a.lo[o] = mn, a.hi[o] = mx;
+            __syncthreads();
+            if (!more) break;
+            u = un;
+            L = Ln;
+            continue;
+        }
+        if (n >= a.min_count && n > 0) {   // block-uniform
+            int i0, j0, i1, j1;
+            double g0, g1;
+            qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
+            qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
+            const int kl = j0, ku = n - 1 - i1;        // largest ranks needed from either end
+            const int ql = kl / LNW + 1, qu = ku / LNW + 1;
+            ok = ql <= WAVE && qu <= WAVE;
+            uint64_t tl = SENT, tu = SENT;
             if (ok) {
-                int ol = off & 0xFFFF, oh = off >> 16;
-#pragma unroll
-                for (int v = 0; v < VPT; ++v) {
-                    double x = xv[v];
-                    asm volatile("" : "+v"(x));   // recompute (no SGPR masks kept from the count)
-                    if (x < tlo) sm.cand[0][ol++] = dkey(x);
-                    if (x > thi) sm.cand[1][oh++] = ~dkey(x);
+                uint64_t ka[1] = {isnan(mn) ? SENT : dkey(mn)};
+                uint64_t kb[1] = {isnan(mx) ? SENT : ~dkey(mx)};
+                wave_sort<1>(ka);
+                wave_sort<1>(kb);
+                if (lane == 0) {
+                    sm.tw[0][w] = readlane_u64(ka[0], ql - 1);
+                    sm.tw[1][w] = readlane_u64(kb[0], qu - 1);
                 }
                 __syncthreads();
-                if (w < 2) {
+#pragma unroll
+                for (int q = 0; q < LNW; ++q) {
+                    const uint64_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
+                    const int ca = (int)__popcll(__ballot(ka[0] != SENT && ka[0] <= Ta));
+                    const int cb = (int)__popcll(__ballot(kb[0] != SENT && kb[0] <= Tb));
+                    if (lane == 0) {
+                        sm.cnt[0][q][w] = ca;
+                        sm.cnt[1][q][w] = cb;
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < LNW; ++q) {
+                    int ca = 0, cb = 0;
+#pragma unroll
+                    for (int v = 0; v < LNW; ++v) {
+                        ca += sm.cnt[0][q][v];
+                        cb += sm.cnt[1][q][v];
+                    }
+                    const uint64_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
+                    if (Ta != SENT && ca >= kl + 1 && Ta < tl) tl = Ta;
+                    if (Tb != SENT && cb >= ku + 1 && Tb < tu) tu = Tb;
+                }
+                ok = tl != SENT && tu != SENT;
+            }
+            int clo = 0, chi = 0;
+            if (ok) {
+                const double tlo = kval(tl), thi = kval(~tu);
+                int cc = 0;
+#pragma unroll
+                for (int v = 0; v < VPT; ++v) cc += (xv[v] < tlo ? 1 : 0) + (xv[v] > thi ? 0x10000 : 0);
+                int tot = 0;
+                const int off = block_excl_scan<LNW>(cc, sm.ints, &tot);
+                clo = tot & 0xFFFF;
+                chi = tot >> 16;
+                ok = clo <= LCAP && chi <= LCAP;
+                if (ok) {
+                    int ol = off & 0xFFFF, oh = off >> 16;
+#pragma unroll
+                    for (int v = 0; v < VPT; ++v) {
+                        double x = xv[v];
+                        asm volatile("" : "+v"(x));   // recompute (no SGPR masks kept from the count)
+                        if (x < tlo) sm.cand[0][ol++] = dkey(x);
+                        if (x > thi) sm.cand[1][oh++] = ~dkey(x);
+                    }
+                }
+            }
+            // xv is dead from here on: the next unit's loads fly during the candidate sorts
+            if (more) Ln = load(un);
+            fetched = true;
+            if (ok) {
+                __syncthreads();
+                if (w < 2 && FM_AB_LONG != 2) {   // (2: timing builds only, no sort)
                     uint64_t* buf = sm.cand[w];
                     const int cn = w == 0 ? clo : chi;
                     if (cn <= WAVE) wave_sort_lds<1>(buf, cn);
@@ -321,45 +367,70 @@ __global__ __launch_bounds__(LT, 4) void select_long_kernel(SelArgs a) {
                     else wave_sort_lds<8>(buf, cn);
                 }
                 __syncthreads();
+                const int ci = n - 1 - j1, cj = ku;   // upper ranks in complemented order
+                const uint64_t k0 = i0 < clo ? sm.cand[0][i0] : tl;
+                const uint64_t k1 = j0 < clo ? sm.cand[0][j0] : tl;
+                const uint64_t k3 = ~(ci < chi ? sm.cand[1][ci] : tu);   // rank j1
+                const uint64_t k2 = ~(cj < chi ? sm.cand[1][cj] : tu);   // rank i1
+                lo = qlerp(kval(k0), kval(k1), g0, a.lerp_mode);
+                hi = qlerp(kval(k2), kval(k3), g1, a.lerp_mode);
             }
         }
+        if (more && !fetched) Ln = load(un);
         if (!ok) {   // redone by select_stream_kernel<true>
             if (tid == 0) a.nvalid[o] = -1;
-            return;
+        } else {
+            if (a.center != nullptr) {
+                // Gram pivot: the midpoint of the cuts, else of the finite range, else 0
+                double cen = 0.5 * (lo + hi);
+                if (!isfinite(cen)) {   // block-uniform
+                    const uint64_t m1 = block_min_u64<LNW>(isfinite(mn) ? dkey(mn) : SENT, sm.u64s);
+                    const uint64_t m2 = block_min_u64<LNW>(isfinite(mx) ? ~dkey(mx) : SENT, sm.u64s + LNW);
+                    cen = m1 == SENT || m2 == SENT ? 0.0 : 0.5 * (kval(m1) + kval(~m2));
+                    if (!isfinite(cen)) cen = 0.0;
+                }
+                if (tid == 0) a.center[o] = cen;
+            }
+            if (tid == 0) {
+                a.lo[o] = lo;
+                a.hi[o] = hi;
+                a.nvalid[o] = n;
+            }
         }
-        const int ci = n - 1 - j1, cj = ku;   // upper ranks in complemented order
-        const uint64_t k0 = i0 < clo ? sm.cand[0][i0] : tl;
-        const uint64_t k1 = j0 < clo ? sm.cand[0][j0] : tl;
-        const uint64_t k3 = ~(ci < chi ? sm.cand[1][ci] : tu);   // rank j1
-        const uint64_t k2 = ~(cj < chi ? sm.cand[1][cj] : tu);   // rank i1
-        lo = qlerp(kval(k0), kval(k1), g0, a.lerp_mode);
-        hi = qlerp(kval(k2), kval(k3), g1, a.lerp_mode);
+        __syncthreads();   // LDS state is rewritten by the next unit
+        if (!more) break;
+        u = un;
+        L = Ln;
     }
-    if (a.center != nullptr) {
-        // Gram pivot: the midpoint of the cuts, else of the finite range, else 0
-        double cen = 0.5 * (lo + hi);
-        if (!isfinite(cen)) {   // block-uniform
-            const uint64_t m1 = block_min_u64<LNW>(isfinite(mn) ? dkey(mn) : SENT, sm.u64s);
-            const uint64_t m2 = block_min_u64<LNW>(isfinite(mx) ? ~dkey(mx) : SENT, sm.u64s + LNW);
-            cen = m1 == SENT || m2 == SENT ? 0.0 : 0.5 * (kval(m1) + kval(~m2));
-            if (!isfinite(cen)) cen = 0.0;
-        }
-        if (tid == 0) a.center[o] = cen;
-    }
-    if (tid == 0) {
-        a.lo[o] = lo;
-        a.hi[o] = hi;
-        a.nvalid[o] = n;
-    }
+}
+
+int long_grid(int64_t nunits) {
+    static int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int64_t cap = (int64_t)ncu * FM_LONG_PER_CU;   // resident 512-thread workgroups
+    return (int)(nunits < cap ? nunits : cap);
+}
+
+template <int VPT>
+void launch_long(const SelArgs& a, hipStream_t st) {
+    if (FM_LONG_PERSIST)
+        hipLaunchKernelGGL((select_long_kernel<VPT, true>), dim3(long_grid((int64_t)a.nseg * a.ncols)), dim3(LT), 0,
+                           st, a);
+    else
+        hipLaunchKernelGGL((select_long_kernel<VPT, false>), dim3(a.nseg, a.ncols), dim3(LT), 0, st, a);
 }
 
 int launch_select_long(const SelArgs& a, int max_seg_len, hipStream_t st) {
     const int vpt = (max_seg_len + LT - 1) / LT;
-    const dim3 grid(a.nseg, a.ncols);
-    if (vpt <= 16) hipLaunchKernelGGL(select_long_kernel<16>, grid, dim3(LT), 0, st, a);
-    else if (vpt <= 24) hipLaunchKernelGGL(select_long_kernel<24>, grid, dim3(LT), 0, st, a);
-    else if (vpt <= 32) hipLaunchKernelGGL(select_long_kernel<32>, grid, dim3(LT), 0, st, a);
-    else if (vpt <= LONG_VPT) hipLaunchKernelGGL(select_long_kernel<LONG_VPT>, grid, dim3(LT), 0, st, a);
+    if (vpt <= 16) launch_long<16>(a, st);
+    else if (vpt <= 24) launch_long<24>(a, st);
+    else if (vpt <= 32) launch_long<32>(a, st);
+    else if (vpt <= LONG_VPT) launch_long<LONG_VPT>(a, st);
     else {
         set_error("select long kernel: %d-row segments exceed %d", max_seg_len, LONG_VPT * LT);
         return FM_ETOOBIG;

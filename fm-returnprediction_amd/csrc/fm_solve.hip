@@ -390,10 +390,11 @@ __device__ __forceinline__ double rowsum(double v) {
 
 constexpr int G16 = 16;   // lanes per problem
 
-// 128 threads (two waves, eight problems at a time) at two waves per SIMD: 256 VGPRs (the
-// factorization's register rows and columns fit without spills) and four workgroups per
-// CU, so every month of a 600-month panel is resident at once.
-constexpr int S16T = 128;
+// 192 threads (three waves, twelve problems at a time: a Table-2 month's 11 problems in ONE
+// round, so no wave factors twice) at two waves per SIMD: 256 VGPRs (the factorization's
+// register rows and columns fit without spills); every month of a 600-month panel is
+// resident at once.
+constexpr int S16T = 192;
 constexpr int S16W = S16T / WAVE;
 constexpr int S16_MAXP = 32;   // problems per group held in LDS tables
 __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
@@ -488,6 +489,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         double G[G16];
         gram_row(G);
         const double n = rowbc<0>(G[0]);
+        const double ninv = 1.0 / n;   // one division per lane (centering below multiplies)
         // centered moments: lane i (1 <= i <= K1) holds S row r = i - 1, S[r][c] in row[c]
         const bool srow = i >= 1 && i <= K1;
         double row[G16];
@@ -501,7 +503,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                     return;
                 }
                 const double g0j = rowbc<0>(G[j + 1]);   // G[0][j+1]
-                const double v = srow && j < K1 ? G[j + 1] - G[0] * g0j / n : 0.0;
+                const double v = srow && j < K1 ? G[j + 1] - G[0] * g0j * ninv : 0.0;
                 row[j] = v;
                 if (i == j + 1) sii = v;
                 if (j == K) sxy = v;
@@ -509,7 +511,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                 row[j] = 0.0;
             }
         });
-        const double mu = G[0] / n;   // lane i: mean of its variable
+        const double mu = G[0] * ninv;   // lane i: mean of its variable
         const uint64_t gm = 0xFFFFull << (16 * g);
         uint32_t st = 0;
         if ((__ballot(i >= 1 && i <= K && isinf(gdiag)) & gm) != 0) st |= FM_ST_INF_IN_X;
@@ -536,6 +538,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         }
         // ---- augmented Cholesky of S (pivot r = k sits in lane k + 1)
         bool ok = act0, illc = false;
+        double dinv = 0.0;   // lane k + 1: 1 / L[k][k] (the back substitution multiplies by it)
         static_for<0, G16 - 1>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             if (k >= kw) return;   // wave-uniform: no problem of the wave has pivot k
@@ -556,6 +559,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                 if (go && j <= K) row[j] -= lik * sj;
             });
             if (go) row[k] = i == k + 1 ? lkk : lik;
+            if (i == k + 1) dinv = rinv;
         });
         // lanes of a live, unskipped problem with a collapsed pivot: rank deficient
         const bool rank_def = act0 && !ok;
@@ -577,7 +581,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         static_for<0, G16 - 1>([&](auto jc) {
             constexpr int j = 14 - decltype(jc)::value;   // descending
             if (j >= kw) return;   // wave-uniform
-            const double bj = rowbc<j + 1>(t) / rowbc<j + 1>(col[j]);
+            const double bj = rowbc<j + 1>(t) * rowbc<j + 1>(dinv);   // t_j / L[j][j]
             if (ok && j < K) {
                 if (i == j + 1) t = bj;
                 else if (i >= 1 && i - 1 < j) t -= col[j] * bj;

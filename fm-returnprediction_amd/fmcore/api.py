@@ -73,13 +73,8 @@ def summary_from_device(mean, se, tstat, nobs, predictor_cols, k_slope0=1, k_r2=
 def records_summary(values, nw_lags=4):
     """Device FM summaries of the columns of a [T, k] host array (all rows present)."""
     dev = E.require_device()
-    T, k = values.shape
-    rec = torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64)).to(dev).view(T, 1, k)
-    status = torch.full((T, 1), L.FM_ST_FITTED, dtype=torch.int32, device=dev)
-    ix = E.ts_compact(status, 1, 1, T, 1)
-    s = E.ts_summary(rec, k, k, ix, T, 1, k, nw_lags)
-    return (s.mean[0].cpu().numpy(), s.se[0].cpu().numpy(), s.tstat[0].cpu().numpy(),
-            s.nobs[0].cpu().numpy())
+    return records_summary_device(torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64)).to(dev),
+                                  nw_lags)
 
 
 def records_summary_device(vals, nw_lags=0):

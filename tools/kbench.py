@@ -18,6 +18,8 @@ def child():
     from fmcore import lewellen as LW
     dev = E.require_device()
     panel = E.panel_synthetic(600, 5000, 1, device=dev)
+    if os.environ.get("KB_CHUNK"):   # Gram chunk-size A/B (rows per workgroup)
+        panel.chunk_rows = int(os.environ["KB_CHUNK"])
     cfg = LW.PipelineConfig()
     for _ in range(3):
         LW.run_pipeline(panel, cfg)
@@ -41,7 +43,8 @@ def main():
             print(lib, "FAILED", r.stderr[-2000:])
             continue
         d = json.loads(line[0][3:])
-        print(os.path.basename(lib), " ".join(f"{k}={v * 1e3:.1f}us" for k, v in d.items()), flush=True)
+        tag = os.path.basename(os.path.dirname(lib)) + (f"[chunk {os.environ['KB_CHUNK']}]" if os.environ.get("KB_CHUNK") else "")
+        print(tag, " ".join(f"{k}={v * 1e3:.1f}us" for k, v in d.items()), flush=True)
 
 
 if __name__ == "__main__":
