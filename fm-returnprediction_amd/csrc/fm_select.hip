@@ -25,13 +25,7 @@
 #define FM_SELECT_STREAM_VPT 24   // values per thread above which fm_select streams the units
 #endif
 #ifndef FM_AB_LONG
-#define FM_AB_LONG 0              // timing builds only: 1 loads + count, 2 no candidate sort
-#endif
-#ifndef FM_LONG_PERSIST
-#define FM_LONG_PERSIST 0         // 1: persistent grid, next unit prefetched (timing builds: slower)
-#endif
-#ifndef FM_LONG_PER_CU
-#define FM_LONG_PER_CU 1
+#define FM_AB_LONG 0              // timing builds only: 1 loads + count, 2 no candidate select
 #endif
 #ifndef FM_AB_SELECT_STREAM
 #define FM_AB_SELECT_STREAM 0     // timing builds only: the streaming kernel for every long unit
@@ -71,8 +65,7 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
 }
 
 // Segments past the register budget (> 20,480 rows: a daily-frequency panel, a huge
-// cross-section; > 6,144 rows with a row mask or moments; the units the long-segment kernel
-// marked): one workgroup per (segment, column) STREAMS the segment from HBM for every pass instead of holding it in registers -- count / key range, the adaptive
+// cross-section; > 6,144 rows with moments; the units the long-segment kernel marked): one workgroup per (segment, column) STREAMS the segment from HBM for every pass instead of holding it in registers -- count / key range, the adaptive
 // histogram (hist_select: one histogram pass per level, one compaction pass), then the
 // moments if asked.  Exact order statistics, same lerps, same pivot as the register paths.
 __device__ __forceinline__ void stream_unit(const SelArgs& a, int s, int c, SelSmem& sm) {
@@ -201,236 +194,255 @@ __global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
 // Long segments (6,145 .. 20,480 rows: C5's 20,000-firm months, a daily panel's short
 // windows): one 512-thread workgroup per (segment, column) holds the unit in registers
 // (VPT <= 40 values per thread, ONE coalesced HBM read of the unit).  Both winsorize tails:
-//   * per wave, the 64 thread minima (keys) sorted; T_w = the wave's q-th smallest,
-//     q = ceil((k+1)/8) for the largest needed rank k.  With c(T) = the number of valid
-//     thread minima <= T (ballots, every wave x every T_w), tau = the smallest T_w with
-//     c(tau) >= k+1: then k+1 threads own a value <= tau, so s[k] <= tau, and only the
-//     values < tau (a little more than k of them) can precede it;
-//   * those candidates are compacted to LDS (one block scan, both tails at once) and one
-//     wave per tail sorts them; a rank >= the candidate count is tau itself.
-// Units it cannot finish (ranks >= 512, > 512 candidates, too few valid thread minima) are
-// marked (nvalid = -1) and redone by the streaming kernel's fallback pass.  At <= 128 VGPRs
-// (4 waves per SIMD) two workgroups share a CU, so one unit's loads fly while the other
-// selects.
+//   * thresholds on the 32-bit HIGH words of the order-preserving keys: per wave the 64
+//     thread minima's high words sorted, T_w = the wave's q-th smallest, q = ceil((k+1)/8)
+//     for the largest needed rank k; c(T) = the valid thread minima with high word <= T
+//     (ballots, summed over the waves by LDS atomics); tau = the smallest T_w with
+//     c(tau) >= k+1.  The candidates -- every value whose high word is <= tau -- are then a
+//     PREFIX of the sorted values holding at least k+1 of them, so the order statistics are
+//     ranks inside the candidates (the upper tail the same on complemented keys);
+//   * both tails' candidates (a little more than 2k values) are compacted to LDS with one
+//     block scan; each wave sorts one 64-key run of each tail and every candidate finds its
+//     merged rank by binary searches in the other runs, so the whole workgroup works on the
+//     order statistics (no single-wave sort of hundreds of keys).
+// Units it cannot finish (ranks >= 512, > 512 candidates per tail, too few valid thread
+// minima) are marked (nvalid = -1) and redone by the streaming kernel's fallback pass.  At
+// <= 128 VGPRs (4 waves per SIMD) two workgroups share a CU, so one unit's loads fly while
+// the other selects.
 constexpr int LT = 512;
 constexpr int LNW = LT / WAVE;
 constexpr int LONG_VPT = 40;
 constexpr int LCAP = 8 * WAVE;   // candidates per tail
 
 struct LongSmem {
-    uint64_t cand[2][LCAP];      // [lower / upper] candidate keys (upper: complemented)
-    uint64_t tw[2][LNW];         // per-wave thresholds T_w
-    int cnt[2][LNW][LNW];        // [tail][threshold][wave]: valid minima <= threshold
-    int ints[LNW];
-    uint64_t u64s[2 * LNW];
+    double cand[2 * LCAP];       // lower-tail candidates, then upper-tail ones at LCAP
+    SelSmemT<LNW> hs;            // hist_select scratch (and the block reductions)
+    uint32_t tw[2][LNW];         // per-wave thresholds T_w (high words)
+    int tot[2][LNW];             // c(T_w), summed over the waves
+    uint64_t res[4];             // keys of the four order statistics
 };
 
-// PERSIST: one workgroup per CU (<= 256 VGPRs: the prefetched unit and the candidate sort
-// live together without spills) walks the units; the next unit's loads are issued as soon
-// as this unit's candidates sit in LDS, so they fly during the candidate sorts.
-template <int VPT, bool PERSIST>
-__global__ __launch_bounds__(LT, PERSIST ? 2 : 4) void select_long_kernel(SelArgs a) {
+// MID: any ranks (pandas' 20% / 50% NYSE breakpoints, row masks): the adaptive histogram
+// select runs over the register-held values directly (no tail thresholds).
+template <int VPT, bool MID>
+__global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a) {
     __shared__ LongSmem sm;
     const int tid = (int)threadIdx.x, lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
-    const int64_t nunits = (int64_t)a.nseg * a.ncols;
-    int64_t u = PERSIST ? (int64_t)blockIdx.x : (int64_t)blockIdx.y * a.nseg + blockIdx.x;
-    if (u >= nunits) return;   // block-uniform
+    const int s = blockIdx.x, c = blockIdx.y;
+    const int64_t o = (int64_t)c * a.nseg + s;
+    const int64_t r0 = a.seg_off[s];
+    const int L = (int)(a.seg_off[s + 1] - r0);
     typedef const __attribute__((address_space(1))) char* gptr;
+    const gptr src = (gptr)(a.cols + (int64_t)c * a.col_stride + r0);
+    const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
     uint32_t lb = (uint32_t)tid * 8u;
     asm volatile("" : "+v"(lb));
     double xv[VPT];
-    auto load = [&](int64_t uu) -> int {   // unconditional (clamped) loads, masked at use
-        const int s = (int)(uu % a.nseg), c = (int)(uu / a.nseg);
-        const int64_t r0 = a.seg_off[s];
-        const int L = (int)(a.seg_off[s + 1] - r0);
-        const gptr src = (gptr)(a.cols + (int64_t)c * a.col_stride + r0);
-        const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
+    if (!MID || a.mask == nullptr) {   // block-uniform
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {   // unconditional (clamped) loads, masked after
+            const uint32_t off = lb + (uint32_t)(v * LT * 8);
+            const double x = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
+            xv[v] = off <= lastb && L > 0 ? x : NAN;
+        }
+    } else {
+        const gptr mb = (gptr)(a.mask + r0);
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
             const uint32_t off = lb + (uint32_t)(v * LT * 8);
-            xv[v] = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
+            const uint32_t oc = off < lastb ? off : lastb;
+            const double x = *(const __attribute__((address_space(1))) double*)(src + oc);
+            const uint8_t m = *(mb + (oc >> 3));
+            xv[v] = off <= lastb && L > 0 && m != 0 ? x : NAN;
         }
-        return L;
-    };
-    int L = load(u);
-    while (true) {
-        const int64_t un = u + gridDim.x;
-        const bool more = PERSIST && un < nunits;   // block-uniform
-        int Ln = 0;
-        bool fetched = false;
-        const int s = (int)(u % a.nseg), c = (int)(u / a.nseg);
-        const int64_t o = (int64_t)c * a.nseg + s;
-        {
-            const uint32_t lastb = (uint32_t)(L > 0 ? L - 1 : 0) * 8u;
+    }
+    int cnt = 0;
+    double mn = NAN, mx = NAN;
 #pragma unroll
-            for (int v = 0; v < VPT; ++v)
-                if (!(lb + (uint32_t)(v * LT * 8) <= lastb && L > 0)) xv[v] = NAN;
-        }
-        int cnt = 0;
-        double mn = NAN, mx = NAN;
+    for (int v = 0; v < VPT; ++v) {
+        cnt += isnan(xv[v]) ? 0 : 1;
+        mn = hw_min(mn, xv[v]);
+        mx = hw_max(mx, xv[v]);
+    }
+    if (tid < 2 * LNW) sm.tot[tid / LNW][tid % LNW] = 0;
+    const int n = block_sum<LNW>(cnt, sm.hs.ints);
+    double lo = NAN, hi = NAN;
+    if (FM_AB_LONG == 1) {   // timing builds only: the load + count floor
+        if (tid == 0) a.nvalid[o] = n, a.lo[o] = mn, a.hi[o] = mx;
+        return;
+    }
+    bool ok = true;
+    if (MID && n >= a.min_count && n > 0) {   // block-uniform
+        int rk[4];
+        double g0, g1;
+        qranks(n, a.q_lo, a.lerp_mode, rk[0], rk[1], g0);
+        qranks(n, a.q_hi, a.lerp_mode, rk[2], rk[3], g1);
+        uint64_t kmn = SENT, kmx = 0;
 #pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-            cnt += isnan(xv[v]) ? 0 : 1;
-            mn = hw_min(mn, xv[v]);
-            mx = hw_max(mx, xv[v]);
-        }
-        const int n = block_sum<LNW>(cnt, sm.ints);
-        double lo = NAN, hi = NAN;
-        bool ok = true;
-        if (FM_AB_LONG == 1) {   // timing builds only: the load + count floor
-            if (more) Ln = load(un);
-            if (tid == 0) a.nvalid[o] = n, a.lo[o] = mn, a.hi[o] = mx;
+        for (int v = 0; v < VPT; ++v)
+            if (!isnan(xv[v])) {
+                const uint64_t k = dkey(xv[v]);
+                kmn = k < kmn ? k : kmn;
+                kmx = k > kmx ? k : kmx;
+            }
+        kmn = block_min_u64<LNW>(kmn, sm.hs.u64s);
+        kmx = block_max_u64<LNW>(kmx, sm.hs.u64s + LNW);
+        uint64_t ko[4];
+        hist_select_t<LNW, HB, HCAP>([&](auto&& f) {
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) f(xv[v]);
+        }, 4, rk, kmn, kmx, ko, sm.hs);
+        lo = qlerp(kval(ko[0]), kval(ko[1]), g0, a.lerp_mode);
+        hi = qlerp(kval(ko[2]), kval(ko[3]), g1, a.lerp_mode);
+    } else if (!MID && n >= a.min_count && n > 0) {   // block-uniform
+        int i0, j0, i1, j1;
+        double g0, g1;
+        qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
+        qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
+        const int kl = j0, ku = n - 1 - i1;        // largest ranks needed from either end
+        const int ql = kl / LNW + 1, qu = ku / LNW + 1;
+        ok = ql <= WAVE && qu <= WAVE;
+        uint32_t tl = 0xFFFFFFFFu, tu = 0xFFFFFFFFu;
+        if (ok) {
+            // high words of the thread extrema's keys (NaN thread: 0xFFFFFFFF, above every
+            // valid key's high word)
+            uint32_t ha[1] = {isnan(mn) ? 0xFFFFFFFFu : (uint32_t)(dkey(mn) >> 32)};
+            uint32_t hb[1] = {isnan(mx) ? 0xFFFFFFFFu : (uint32_t)(~dkey(mx) >> 32)};
+            const uint32_t ua = ha[0], ub = hb[0];
+            wave_sort32<1>(ha);
+            wave_sort32<1>(hb);
+            if (lane == 0) {
+                sm.tw[0][w] = (uint32_t)__builtin_amdgcn_readlane((int)ha[0], ql - 1);
+                sm.tw[1][w] = (uint32_t)__builtin_amdgcn_readlane((int)hb[0], qu - 1);
+            }
             __syncthreads();
-            if (!more) break;
-            u = un;
-            L = Ln;
-            continue;
-        }
-        if (n >= a.min_count && n > 0) {   // block-uniform
-            int i0, j0, i1, j1;
-            double g0, g1;
-            qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
-            qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
-            const int kl = j0, ku = n - 1 - i1;        // largest ranks needed from either end
-            const int ql = kl / LNW + 1, qu = ku / LNW + 1;
-            ok = ql <= WAVE && qu <= WAVE;
-            uint64_t tl = SENT, tu = SENT;
-            if (ok) {
-                uint64_t ka[1] = {isnan(mn) ? SENT : dkey(mn)};
-                uint64_t kb[1] = {isnan(mx) ? SENT : ~dkey(mx)};
-                wave_sort<1>(ka);
-                wave_sort<1>(kb);
+#pragma unroll
+            for (int q = 0; q < LNW; ++q) {
+                const uint32_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
+                const int ca = (int)__popcll(__ballot(ua != 0xFFFFFFFFu && ua <= Ta));
+                const int cb = (int)__popcll(__ballot(ub != 0xFFFFFFFFu && ub <= Tb));
                 if (lane == 0) {
-                    sm.tw[0][w] = readlane_u64(ka[0], ql - 1);
-                    sm.tw[1][w] = readlane_u64(kb[0], qu - 1);
-                }
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < LNW; ++q) {
-                    const uint64_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
-                    const int ca = (int)__popcll(__ballot(ka[0] != SENT && ka[0] <= Ta));
-                    const int cb = (int)__popcll(__ballot(kb[0] != SENT && kb[0] <= Tb));
-                    if (lane == 0) {
-                        sm.cnt[0][q][w] = ca;
-                        sm.cnt[1][q][w] = cb;
-                    }
-                }
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < LNW; ++q) {
-                    int ca = 0, cb = 0;
-#pragma unroll
-                    for (int v = 0; v < LNW; ++v) {
-                        ca += sm.cnt[0][q][v];
-                        cb += sm.cnt[1][q][v];
-                    }
-                    const uint64_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
-                    if (Ta != SENT && ca >= kl + 1 && Ta < tl) tl = Ta;
-                    if (Tb != SENT && cb >= ku + 1 && Tb < tu) tu = Tb;
-                }
-                ok = tl != SENT && tu != SENT;
-            }
-            int clo = 0, chi = 0;
-            if (ok) {
-                const double tlo = kval(tl), thi = kval(~tu);
-                int cc = 0;
-#pragma unroll
-                for (int v = 0; v < VPT; ++v) cc += (xv[v] < tlo ? 1 : 0) + (xv[v] > thi ? 0x10000 : 0);
-                int tot = 0;
-                const int off = block_excl_scan<LNW>(cc, sm.ints, &tot);
-                clo = tot & 0xFFFF;
-                chi = tot >> 16;
-                ok = clo <= LCAP && chi <= LCAP;
-                if (ok) {
-                    int ol = off & 0xFFFF, oh = off >> 16;
-#pragma unroll
-                    for (int v = 0; v < VPT; ++v) {
-                        double x = xv[v];
-                        asm volatile("" : "+v"(x));   // recompute (no SGPR masks kept from the count)
-                        if (x < tlo) sm.cand[0][ol++] = dkey(x);
-                        if (x > thi) sm.cand[1][oh++] = ~dkey(x);
-                    }
+                    atomicAdd(&sm.tot[0][q], ca);
+                    atomicAdd(&sm.tot[1][q], cb);
                 }
             }
-            // xv is dead from here on: the next unit's loads fly during the candidate sorts
-            if (more) Ln = load(un);
-            fetched = true;
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < LNW; ++q) {
+                const uint32_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
+                if (Ta != 0xFFFFFFFFu && sm.tot[0][q] >= kl + 1 && Ta < tl) tl = Ta;
+                if (Tb != 0xFFFFFFFFu && sm.tot[1][q] >= ku + 1 && Tb < tu) tu = Tb;
+            }
+            ok = tl != 0xFFFFFFFFu && tu != 0xFFFFFFFFu;
+        }
+        int clo = 0, chi = 0;
+        if (ok) {
+            // candidates by value compares against the largest / smallest double of the
+            // threshold high word (+-inf at the ends, where the next keys would be NaNs);
+            // value compares also take the other zero of a +-0 boundary, which keeps the
+            // candidates a prefix / suffix of the sorted values
+            const uint64_t kla = ((uint64_t)tl << 32) | 0xFFFFFFFFull;
+            const uint64_t kub = ~(((uint64_t)tu << 32) | 0xFFFFFFFFull);
+            const double tlo = kla >= dkey(INFINITY) ? INFINITY : kval(kla);
+            const double thi = kub <= dkey(-INFINITY) ? -INFINITY : kval(kub);
+            int cc = 0;
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) cc += (xv[v] <= tlo ? 1 : 0) + (xv[v] >= thi ? 0x10000 : 0);
+            int tot = 0;
+            const int off = block_excl_scan<LNW>(cc, sm.hs.ints, &tot);
+            clo = tot & 0xFFFF;
+            chi = tot >> 16;
+            // caps, and the rare overlap of the two sets (massive ties): redone by the fallback
+            ok = clo <= LCAP && chi <= LCAP && clo + chi <= n && clo > kl && chi > ku;
             if (ok) {
-                __syncthreads();
-                if (w < 2 && FM_AB_LONG != 2) {   // (2: timing builds only, no sort)
-                    uint64_t* buf = sm.cand[w];
-                    const int cn = w == 0 ? clo : chi;
-                    if (cn <= WAVE) wave_sort_lds<1>(buf, cn);
-                    else if (cn <= 2 * WAVE) wave_sort_lds<2>(buf, cn);
-                    else if (cn <= 4 * WAVE) wave_sort_lds<4>(buf, cn);
-                    else wave_sort_lds<8>(buf, cn);
+                int ol = off & 0xFFFF, oh = LCAP + (off >> 16);
+#pragma unroll
+                for (int v = 0; v < VPT; ++v) {
+                    double x = xv[v];
+                    asm volatile("" : "+v"(x));   // recompute (no SGPR masks kept from the count)
+                    if (x <= tlo) sm.cand[ol++] = x;
+                    if (x >= thi) sm.cand[oh++] = x;
                 }
                 __syncthreads();
-                const int ci = n - 1 - j1, cj = ku;   // upper ranks in complemented order
-                const uint64_t k0 = i0 < clo ? sm.cand[0][i0] : tl;
-                const uint64_t k1 = j0 < clo ? sm.cand[0][j0] : tl;
-                const uint64_t k3 = ~(ci < chi ? sm.cand[1][ci] : tu);   // rank j1
-                const uint64_t k2 = ~(cj < chi ? sm.cand[1][cj] : tu);   // rank i1
-                lo = qlerp(kval(k0), kval(k1), g0, a.lerp_mode);
-                hi = qlerp(kval(k2), kval(k3), g1, a.lerp_mode);
+                // the four order statistics among the candidates: wave w sorts run w of each
+                // tail (64 keys; the upper tail on complemented keys, so both count from their
+                // end), then every candidate's merged rank = its run position + the entries
+                // of the other runs before it (binary searches, ties by run); the lanes at
+                // the target ranks store their keys
+                uint64_t* ck = reinterpret_cast<uint64_t*>(sm.cand);
+                const int e = w * WAVE + lane;
+                uint64_t ka[1] = {e < clo ? dkey(sm.cand[e]) : SENT};
+                uint64_t kb[1] = {e < chi ? ~dkey(sm.cand[LCAP + e]) : SENT};
+                if (FM_AB_LONG != 2) {
+                    wave_sort<1>(ka);
+                    wave_sort<1>(kb);
+                }
+                ck[e] = ka[0];   // in place: wave w owns entries [64 w, 64 w + 64) of each list
+                ck[LCAP + e] = kb[0];
+                if (tid < 4) sm.res[tid] = SENT;
+                __syncthreads();
+                const int nrl = (clo + WAVE - 1) / WAVE, nru = (chi + WAVE - 1) / WAVE;
+                if (ka[0] != SENT) {
+                    int r = lane;
+                    for (int u = 0; u < nrl; ++u)
+                        if (u != w) r += merge_count(ck + u * WAVE, ka[0], u < w);
+                    if (r == i0) sm.res[0] = ka[0];
+                    if (r == j0) sm.res[1] = ka[0];
+                }
+                if (kb[0] != SENT) {
+                    int r = lane;
+                    for (int u = 0; u < nru; ++u)
+                        if (u != w) r += merge_count(ck + LCAP + u * WAVE, kb[0], u < w);
+                    if (r == n - 1 - i1) sm.res[2] = ~kb[0];
+                    if (r == n - 1 - j1) sm.res[3] = ~kb[0];
+                }
+                __syncthreads();
+                lo = qlerp(kval(sm.res[0]), kval(sm.res[1]), g0, a.lerp_mode);
+                hi = qlerp(kval(sm.res[2]), kval(sm.res[3]), g1, a.lerp_mode);
             }
         }
-        if (more && !fetched) Ln = load(un);
-        if (!ok) {   // redone by select_stream_kernel<true>
-            if (tid == 0) a.nvalid[o] = -1;
-        } else {
-            if (a.center != nullptr) {
-                // Gram pivot: the midpoint of the cuts, else of the finite range, else 0
-                double cen = 0.5 * (lo + hi);
-                if (!isfinite(cen)) {   // block-uniform
-                    const uint64_t m1 = block_min_u64<LNW>(isfinite(mn) ? dkey(mn) : SENT, sm.u64s);
-                    const uint64_t m2 = block_min_u64<LNW>(isfinite(mx) ? ~dkey(mx) : SENT, sm.u64s + LNW);
-                    cen = m1 == SENT || m2 == SENT ? 0.0 : 0.5 * (kval(m1) + kval(~m2));
-                    if (!isfinite(cen)) cen = 0.0;
-                }
-                if (tid == 0) a.center[o] = cen;
-            }
-            if (tid == 0) {
-                a.lo[o] = lo;
-                a.hi[o] = hi;
-                a.nvalid[o] = n;
-            }
+    }
+    if (!ok) {   // redone by select_stream_kernel<true>
+        if (tid == 0) a.nvalid[o] = -1;
+        return;
+    }
+    if (a.center != nullptr) {
+        // Gram pivot: the midpoint of the cuts, else of the finite range, else 0
+        double cen = 0.5 * (lo + hi);
+        if (!isfinite(cen)) {   // block-uniform
+            const uint64_t m1 = block_min_u64<LNW>(isfinite(mn) ? dkey(mn) : SENT, sm.hs.u64s);
+            const uint64_t m2 = block_min_u64<LNW>(isfinite(mx) ? ~dkey(mx) : SENT, sm.hs.u64s + LNW);
+            cen = m1 == SENT || m2 == SENT ? 0.0 : 0.5 * (kval(m1) + kval(~m2));
+            if (!isfinite(cen)) cen = 0.0;
         }
-        __syncthreads();   // LDS state is rewritten by the next unit
-        if (!more) break;
-        u = un;
-        L = Ln;
+        if (tid == 0) a.center[o] = cen;
+    }
+    if (tid == 0) {
+        a.lo[o] = lo;
+        a.hi[o] = hi;
+        a.nvalid[o] = n;
     }
 }
 
-int long_grid(int64_t nunits) {
-    static int ncu = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return n;
-    }();
-    const int64_t cap = (int64_t)ncu * FM_LONG_PER_CU;   // resident 512-thread workgroups
-    return (int)(nunits < cap ? nunits : cap);
-}
-
 template <int VPT>
-void launch_long(const SelArgs& a, hipStream_t st) {
-    if (FM_LONG_PERSIST)
-        hipLaunchKernelGGL((select_long_kernel<VPT, true>), dim3(long_grid((int64_t)a.nseg * a.ncols)), dim3(LT), 0,
-                           st, a);
+void launch_long(const SelArgs& a, hipStream_t st, bool mid) {
+    if (mid)
+        hipLaunchKernelGGL((select_long_kernel<VPT, true>), dim3(a.nseg, a.ncols), dim3(LT), 0, st, a);
     else
         hipLaunchKernelGGL((select_long_kernel<VPT, false>), dim3(a.nseg, a.ncols), dim3(LT), 0, st, a);
 }
 
 int launch_select_long(const SelArgs& a, int max_seg_len, hipStream_t st) {
     const int vpt = (max_seg_len + LT - 1) / LT;
-    if (vpt <= 16) launch_long<16>(a, st);
-    else if (vpt <= 24) launch_long<24>(a, st);
-    else if (vpt <= 32) launch_long<32>(a, st);
-    else if (vpt <= LONG_VPT) launch_long<LONG_VPT>(a, st);
+    // the tail thresholds serve ranks < 512 from either end; row masks and middle ranks
+    // take the histogram over all values
+    const double span = (double)(max_seg_len > 0 ? max_seg_len - 1 : 0);
+    const bool mid = a.mask != nullptr || a.q_lo * span + 2.0 > (double)LT || (1.0 - a.q_hi) * span + 2.0 > (double)LT;
+    if (vpt <= 16) launch_long<16>(a, st, mid);
+    else if (vpt <= 24) launch_long<24>(a, st, mid);
+    else if (vpt <= 32) launch_long<32>(a, st, mid);
+    else if (vpt <= LONG_VPT) launch_long<LONG_VPT>(a, st, mid);
     else {
         set_error("select long kernel: %d-row segments exceed %d", max_seg_len, LONG_VPT * LT);
         return FM_ETOOBIG;
@@ -960,8 +972,8 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
               x.min_count, x.lerp_mode,  x.lo,    x.hi,     x.nvalid, x.mean, x.sd,  x.center};
     hipStream_t st = (hipStream_t)stream;
     const int vpt = (max_seg_len + ST - 1) / ST;
-    if (vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && row_mask == nullptr &&
-        x.mean == nullptr && nvalid != nullptr && !FM_AB_SELECT_STREAM) {
+    if (vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && x.mean == nullptr && nvalid != nullptr &&
+        !FM_AB_SELECT_STREAM) {
         // past the 256-thread paths' register budget: the 512-thread register-resident
         // kernel (one read per unit); the streaming kernel redoes the units it marked
         const int rc = launch_select_long(a, max_seg_len, st);
