@@ -433,12 +433,16 @@ void launch_long(const SelArgs& a, hipStream_t st, bool mid) {
         hipLaunchKernelGGL((select_long_kernel<VPT, false>), dim3(a.nseg, a.ncols), dim3(LT), 0, st, a);
 }
 
+// the tail thresholds serve ranks < 512 from either end; row masks and middle ranks take the
+// histogram over all values (the MID kernel)
+bool long_is_mid(const SelArgs& a, int max_seg_len) {
+    const double span = (double)(max_seg_len > 0 ? max_seg_len - 1 : 0);
+    return a.mask != nullptr || a.q_lo * span + 2.0 > (double)LT || (1.0 - a.q_hi) * span + 2.0 > (double)LT;
+}
+
 int launch_select_long(const SelArgs& a, int max_seg_len, hipStream_t st) {
     const int vpt = (max_seg_len + LT - 1) / LT;
-    // the tail thresholds serve ranks < 512 from either end; row masks and middle ranks
-    // take the histogram over all values
-    const double span = (double)(max_seg_len > 0 ? max_seg_len - 1 : 0);
-    const bool mid = a.mask != nullptr || a.q_lo * span + 2.0 > (double)LT || (1.0 - a.q_hi) * span + 2.0 > (double)LT;
+    const bool mid = long_is_mid(a, max_seg_len);
     if (vpt <= 16) launch_long<16>(a, st, mid);
     else if (vpt <= 24) launch_long<24>(a, st, mid);
     else if (vpt <= 32) launch_long<32>(a, st, mid);
@@ -968,8 +972,10 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
     FM_REQUIRE(x.q_lo >= 0.0 && x.q_lo <= 1.0 && x.q_hi >= 0.0 && x.q_hi <= 1.0,
                "fm_select_cuts: quantiles must be in [0,1]");
     if (nseg == 0) return FM_OK;
+    FM_REQUIRE(x.level == nullptr || ncols == 1, "fm_select: level needs a single column");
     SelArgs a{cols,        x.col_stride, seg_off, nseg,     ncols, row_mask, x.q_lo, x.q_hi,
-              x.min_count, x.lerp_mode,  x.lo,    x.hi,     x.nvalid, x.mean, x.sd,  x.center};
+              x.min_count, x.lerp_mode,  x.lo,    x.hi,     x.nvalid, x.mean, x.sd,  x.center,
+              nullptr,     x.level};
     hipStream_t st = (hipStream_t)stream;
     const int vpt = (max_seg_len + ST - 1) / ST;
     if (vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && x.mean == nullptr && nvalid != nullptr &&
@@ -981,14 +987,18 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
         FM_CHECK_LAUNCH("fm_select_cuts(long)");
         hipLaunchKernelGGL(select_stream_kernel<true>, dim3(256), dim3(ST), 0, st, a);
         FM_CHECK_LAUNCH("fm_select_cuts(long fallback)");
-        return FM_OK;
+        // the level bytes by a streaming launch: writing them from the select kernel (a
+        // re-read of the unmasked column, or unmasked registers + mask bits) measured no
+        // faster, the register select being latency-bound at one workgroup per CU
+        return a.level ? fm_universe_level(cols, seg_off, nseg, (int64_t)max_seg_len * nseg, x.lo, x.hi, x.level, stream)
+                       : FM_OK;
     }
     if (vpt > FM_SELECT_STREAM_VPT) {
         // longer still, or row masks / moments: stream every unit from HBM / L2 for each
         // pass (exact, any length)
         hipLaunchKernelGGL(select_stream_kernel<false>, dim3(nseg, ncols), dim3(ST), 0, st, a);
         FM_CHECK_LAUNCH("fm_select_cuts(stream)");
-        return FM_OK;
+        return a.level ? fm_universe_level(cols, seg_off, nseg, (int64_t)max_seg_len * nseg, x.lo, x.hi, x.level, stream) : FM_OK;
     }
     // wave fast path: no row mask, segments of <= 96 * 64 rows, nvalid present (it carries
     // the fallback marks); the workgroup kernel then redoes the marked units only
@@ -1030,7 +1040,7 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
     else if (vpt <= 64) launch_select<64>(a, ncols, st, wave);
     else launch_select<96>(a, ncols, st, wave);
     FM_CHECK_LAUNCH("fm_select_cuts");
-    return FM_OK;
+    return a.level ? fm_universe_level(cols, seg_off, nseg, (int64_t)max_seg_len * nseg, x.lo, x.hi, x.level, stream) : FM_OK;
 }
 
 extern "C" int fm_universe(const double* me, const uint8_t* nyse, const int64_t* seg_off, int32_t nseg,

@@ -59,6 +59,7 @@ struct SelArgs {
     double* sd;
     double* center;
     double* prm;   // optional LDS [3][32]: thread 0 also stores lo, hi, center of column c there
+    uint8_t* level;   // fm_select_args.level (written by fm_universe_level after the cuts)
 };
 
 __device__ __forceinline__ uint64_t key_of(double x) { return isnan(x) ? SENT : dkey(x); }

@@ -27,21 +27,38 @@ namespace {
 constexpr int TT = 256;
 constexpr int TNW = TT / WAVE;
 
+// Grid (chunks of CB months, problems): a workgroup counts the fitted months before its chunk
+// (a strided pass over the earlier status words) and scans its own chunk (CPT contiguous
+// months per thread), so a 100,000-month series takes one launch of independent workgroups
+// instead of one workgroup scanning the whole series.
+constexpr int CPT = 16;
+constexpr int CB = TT * CPT;
 __global__ __launch_bounds__(TT) void compact_kernel(const uint32_t* status, int64_t s_seg,
                                                      int64_t s_prob, int nseg, int32_t* idx,
                                                      int32_t* count) {
     __shared__ int scr[TNW];
-    const int p = blockIdx.x;
-    int base = 0;
-    for (int s0 = 0; s0 < nseg; s0 += TT) {
-        const int s = s0 + threadIdx.x;
-        const int f = (s < nseg && (status[s * s_seg + p * s_prob] & FM_ST_FITTED)) ? 1 : 0;
-        int tot = 0;
-        const int off = block_excl_scan<TNW>(f, scr, &tot);
-        if (f) idx[(int64_t)p * nseg + base + off] = s;
-        base += tot;
+    const int p = blockIdx.y;
+    const int c0 = blockIdx.x * CB;
+    const uint32_t* sp = status + (int64_t)p * s_prob;
+    int before = 0;
+    for (int s = threadIdx.x; s < c0; s += TT) before += (sp[(int64_t)s * s_seg] & FM_ST_FITTED) ? 1 : 0;
+    before = block_sum<TNW>(before, scr);
+    const int m0 = c0 + (int)threadIdx.x * CPT;
+    uint32_t fm = 0;
+    int loc = 0;
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+        const int s = m0 + j;
+        const bool f = s < nseg && (sp[(int64_t)(s < nseg ? s : 0) * s_seg] & FM_ST_FITTED);
+        fm |= (f ? 1u : 0u) << j;
+        loc += f ? 1 : 0;
     }
-    if (threadIdx.x == 0) count[p] = base;
+    int tot = 0;
+    int pos = before + block_excl_scan<TNW>(loc, scr, &tot);
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+        if ((fm >> j) & 1u) idx[(int64_t)p * nseg + pos++] = m0 + j;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) count[p] = before + tot;
 }
 
 struct SumArgs {
@@ -49,7 +66,7 @@ struct SumArgs {
     int64_t r_seg, r_prob;
     const int32_t* idx;
     const int32_t* count;
-    int nseg, kmax, nw_lags;
+    int nseg, kmax, nw_lags, nprob;
     double* mean;
     double* se;
     double* tstat;
@@ -109,27 +126,336 @@ __global__ __launch_bounds__(TT) void summary_kernel(SumArgs a) {
     }
 }
 
-// One workgroup per (problem, coefficient, chunk of RCH output rows): the chunk's window
-// span is staged in LDS, each output is a direct sum over its window (no running-sum drift).
-constexpr int RCH = 1024;
+// Long series (>= SUM_CHUNKED months), three launches:
+//   summary_gather_kernel  the fitted-month records of every (problem, coefficient) into
+//                          contiguous series work[p][k][0..count) (one row's coefficients are
+//                          adjacent in the records, so a workgroup reads rows x all k)
+//   summary_part_kernel    per (chunk of SCH rows, coefficient, problem): NaN dropped in order,
+//                          y' = x - K_c (K_c = the chunk's first value): m, S1', S2', the
+//                          in-chunk lagged cross sums C'_L and the first / last SUM_MAXLAG y'
+//   summary_combine_kernel per series, the chunks in order: each chunk's sums re-shifted to
+//                          K0 = the series' first value (delta = K_c - K0), the lag pairs that
+//                          straddle chunk boundaries from a ring of the last values so far;
+//                          with d = S1 / n (= mean - K0),
+//                          gamma_0 = S2 - n d^2, gamma_L = C_L - d (A_L + B_L) + (n - L) d^2,
+//                          A_L / B_L = S1 minus the first / last L values -- the Newey-West
+//                          sums of the two-pass formula in one pass over the series.
+// work: [nprob][kmax][nseg] series, then [nprob][kmax][nchunk][SPART] partials.
+constexpr int SCH = 2048;
+constexpr int SPT = SCH / TT;
+constexpr int SUM_MAXLAG = 8;
+constexpr int SPART = 4 + SUM_MAXLAG + 2 * SUM_MAXLAG;   // m, K_c, S1', S2', C'_L, first, last
+constexpr int SUM_CHUNKED = 4096;
+constexpr int GROWS = 64;   // rows per gather workgroup (x kmax coefficients)
+
+__global__ __launch_bounds__(TT) void summary_gather_kernel(SumArgs a) {
+    const int p = blockIdx.y, r0 = blockIdx.x * GROWS;
+    const int cnt = a.count[p];
+    const int32_t* ix = a.idx + (int64_t)p * a.nseg;
+    for (int e = threadIdx.x; e < GROWS * a.kmax; e += TT) {
+        const int r = r0 + e / a.kmax, k = e - (e / a.kmax) * a.kmax;
+        if (r < cnt)
+            a.work[((int64_t)p * a.kmax + k) * a.nseg + r] = a.rec[(int64_t)ix[r] * a.r_seg + (int64_t)p * a.r_prob + k];
+    }
+}
+
+__global__ __launch_bounds__(TT) void summary_part_kernel(SumArgs a) {
+    __shared__ double ys[SCH];
+    __shared__ int ired[TNW];
+    __shared__ double dred[TNW];
+    const int c = blockIdx.x, k = blockIdx.y, p = blockIdx.z;
+    const int cnt = a.count[p];
+    const int c0 = c * SCH;
+    const double* ser = a.work + ((int64_t)p * a.kmax + k) * a.nseg;
+    double* part = a.work + (int64_t)a.nprob * a.kmax * a.nseg +
+                   (((int64_t)p * a.kmax + k) * gridDim.x + c) * SPART;
+    // this chunk's values, SPT contiguous rows per thread, NaN dropped in order
+    const int i0 = c0 + (int)threadIdx.x * SPT;
+    double y[SPT];
+    int loc = 0;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+        const int i = i0 + j;
+        y[j] = i < cnt ? ser[i] : (double)NAN;
+        loc += isnan(y[j]) ? 0 : 1;
+    }
+    int m = 0;
+    int pos = block_excl_scan<TNW>(loc, ired, &m);
+#pragma unroll
+    for (int j = 0; j < SPT; ++j)
+        if (!isnan(y[j])) ys[pos++] = y[j];
+    __syncthreads();
+    const double kc = m > 0 ? ys[0] : 0.0;
+    double s1 = 0.0, s2 = 0.0, cl[SUM_MAXLAG];
+#pragma unroll
+    for (int l = 0; l < SUM_MAXLAG; ++l) cl[l] = 0.0;
+    for (int j = threadIdx.x; j < m; j += TT) {
+        const double v = ys[j] - kc;
+        s1 += v;
+        s2 += v * v;
+#pragma unroll
+        for (int l = 1; l <= SUM_MAXLAG; ++l)
+            if (j - l >= 0) cl[l - 1] += v * (ys[j - l] - kc);
+    }
+    s1 = block_sum<TNW>(s1, dred);
+    s2 = block_sum<TNW>(s2, dred);
+#pragma unroll
+    for (int l = 0; l < SUM_MAXLAG; ++l) {
+        const double t = block_sum<TNW>(cl[l], dred);
+        if (threadIdx.x == 0) part[4 + l] = t;
+    }
+    if (threadIdx.x == 0) {
+        part[0] = (double)m;
+        part[1] = kc;
+        part[2] = s1;
+        part[3] = s2;
+    }
+    if (threadIdx.x < SUM_MAXLAG) {
+        const int t = threadIdx.x;
+        part[4 + SUM_MAXLAG + t] = t < m ? ys[t] - kc : 0.0;                        // first
+        part[4 + 2 * SUM_MAXLAG + t] = t < m ? ys[m - 1 - t] - kc : 0.0;            // last (reversed)
+    }
+}
+
+// One wave per (coefficient, problem): the partials staged in LDS by all lanes, then the
+// chunks in order (see above); mean, Newey-West s.e. and t (weights 1 - L/n, stop at the
+// first negative weight; src/regressions.py:78-100).
+constexpr int SCMAX = 64;   // chunks staged in LDS per pass of the combine
+__global__ __launch_bounds__(WAVE) void summary_combine_kernel(SumArgs a, int nchunk) {
+    __shared__ double stage[SCMAX * SPART];
+    const int k = blockIdx.x, p = blockIdx.y;
+    const int L = a.nw_lags < SUM_MAXLAG ? a.nw_lags : SUM_MAXLAG;
+    const double* gpart = a.work + (int64_t)a.nprob * a.kmax * a.nseg + ((int64_t)p * a.kmax + k) * nchunk * SPART;
+    const double* part = stage;
+    int n = 0;
+    double k0 = NAN, S1 = 0.0, S2 = 0.0, C[SUM_MAXLAG];
+    double head[SUM_MAXLAG], ring[SUM_MAXLAG];   // first values; the last values so far (ring[0] newest)
+    int nhead = 0;
+#pragma unroll
+    for (int l = 0; l < SUM_MAXLAG; ++l) C[l] = head[l] = ring[l] = 0.0;
+    for (int c = 0; c < nchunk; ++c) {
+        if (c % SCMAX == 0) {   // the next SCMAX chunks' partials, all lanes loading
+            __syncthreads();
+            const int nc = nchunk - c < SCMAX ? nchunk - c : SCMAX;
+            for (int e = threadIdx.x; e < nc * SPART; e += WAVE) stage[e] = gpart[(int64_t)c * SPART + e];
+            __syncthreads();
+        }
+        const double* q = part + (int64_t)(c % SCMAX) * SPART;
+        const int m = (int)q[0];
+        if (m == 0) continue;
+        if (n == 0) k0 = q[1];
+        const double dl = q[1] - k0;   // re-shift this chunk's sums from K_c to K0
+        const double s1p = q[2], s2p = q[3];
+        double fsum = 0.0, lsum = 0.0;
+#pragma unroll
+        for (int l = 1; l <= SUM_MAXLAG; ++l) {
+            if (l > L) break;
+            fsum += l - 1 < m ? q[4 + SUM_MAXLAG + l - 1] : 0.0;
+            lsum += l - 1 < m ? q[4 + 2 * SUM_MAXLAG + l - 1] : 0.0;
+            const int pc = m - l > 0 ? m - l : 0;   // in-chunk pairs at lag l
+            double cc = q[4 + l - 1];
+            if (pc > 0) cc += dl * ((s1p - fsum) + (s1p - lsum)) + (double)pc * dl * dl;
+            // pairs (j, j - l) with j < l: partners before this chunk (the ring)
+#pragma unroll
+            for (int j = 0; j < SUM_MAXLAG; ++j)
+                if (j < l && j < m && l - 1 - j < n && l - 1 - j < SUM_MAXLAG)
+                    cc += (q[4 + SUM_MAXLAG + j] + dl) * ring[l - 1 - j];
+            C[l - 1] += cc;
+        }
+        S1 += s1p + (double)m * dl;
+        S2 += s2p + 2.0 * dl * s1p + (double)m * dl * dl;
+        // the global first values; the ring of the last values (shifted to K0)
+#pragma unroll
+        for (int j = 0; j < SUM_MAXLAG; ++j)
+            if (j < m && nhead < SUM_MAXLAG) head[nhead++] = q[4 + SUM_MAXLAG + j] + dl;
+        const int push = m < SUM_MAXLAG ? m : SUM_MAXLAG;
+#pragma unroll
+        for (int j = SUM_MAXLAG - 1; j >= 0; --j)   // older values move back by `push`
+            ring[j] = j - push >= 0 ? ring[j - push] : q[4 + 2 * SUM_MAXLAG + j] + dl;
+        n += m;
+    }
+    double mu = NAN, se = NAN;
+    if (n > 0) {
+        const double d = S1 / (double)n;
+        mu = k0 + d;
+        const double g0 = S2 - (double)n * d * d;
+        double accn = 0.0, hs = 0.0, ts = 0.0;
+#pragma unroll
+        for (int l = 1; l <= SUM_MAXLAG; ++l) {
+            if (l > L) break;
+            const double w = 1.0 - ((double)l / (double)n);
+            if (w < 0.0) break;
+            hs += head[l - 1];   // the first l values
+            ts += ring[l - 1];   // the last l values
+            accn += w * (C[l - 1] - d * ((S1 - hs) + (S1 - ts)) + (double)(n - l) * d * d);
+        }
+        if (n >= 2) se = sqrt((g0 + 2.0 * accn) / ((double)n * (double)n));
+    }
+    if (threadIdx.x == 0) {   // every lane walked the same (LDS-broadcast) partials
+        const int64_t o = (int64_t)p * a.kmax + k;
+        a.mean[o] = mu;
+        a.se[o] = se;
+        a.tstat[o] = mu / se;
+        a.nobs[o] = n;
+    }
+}
+
+// Grid (chunks of RCH output rows, problem): the chunk's window span of ALL coefficients is
+// staged in LDS (a row's coefficients are adjacent in the records: one gather per row, not
+// one per coefficient); thread (k, g) owns coefficient k on RPT consecutive rows: the first
+// output is a direct sum over its window, the next RPT-1 slide it (add the entering row, drop
+// the leaving one; finite values only -- pandas turns +-inf into NaN).
+constexpr int RKMAX = 16;                 // coefficients per problem (pmax <= 16 here)
+constexpr int RKS = RKMAX + 1;            // LDS row stride (odd: the row groups hit other banks)
+constexpr int RPT = 16;                   // rows per thread
+constexpr int RCH = TT / RKMAX * RPT;     // 256 output rows per workgroup
 constexpr int RMAXW = 1024;
+constexpr int RSPAN = RCH + 128;          // staged rows (windows up to 129 here): 52 KB of LDS
 
 __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t r_seg,
                                                      int64_t r_prob, const int32_t* idx,
                                                      const int32_t* count, int nseg, int kmax,
                                                      int window, int minp, double* out) {
-    __shared__ double xs[RCH + RMAXW];
-    const int p = blockIdx.y / kmax, k = blockIdx.y - (blockIdx.y / kmax) * kmax;
+    __shared__ double xs[RSPAN * RKS];
+    const int p = blockIdx.y;
     const int c0 = blockIdx.x * RCH;
     const int cnt = count[p];
     // rows past the fitted-month count have no month: NaN (never left uninitialised)
     const int cend = c0 + RCH < nseg ? c0 + RCH : nseg;
+    for (int e = threadIdx.x; e < (cend - c0) * kmax; e += TT) {
+        const int i = c0 + e / kmax;
+        if (i >= cnt) out[((int64_t)p * nseg + i) * kmax + (e % kmax)] = NAN;
+    }
+    if (c0 >= cnt) return;
+    const int32_t* ix = idx + (int64_t)p * nseg;
+    const int lo = c0 - window + 1 < 0 ? 0 : c0 - window + 1;
+    const int hi = c0 + RCH < cnt ? c0 + RCH : cnt;
+    for (int e = threadIdx.x; e < (hi - lo) * kmax; e += TT) {
+        const int j = lo + e / kmax, k = e % kmax;
+        xs[(j - lo) * RKS + k] = rec[(int64_t)ix[j] * r_seg + (int64_t)p * r_prob + k];
+    }
+    __syncthreads();
+    const int k = threadIdx.x % RKMAX, g = threadIdx.x / RKMAX;
+    const int ib = c0 + g * RPT;
+    if (k >= kmax || ib >= hi) return;
+    const int j0 = ib - window + 1 < 0 ? 0 : ib - window + 1;
+    double sm = 0.0;
+    int c = 0;
+    for (int j = j0; j <= ib; ++j) {
+        const double x = xs[(j - lo) * RKS + k];
+        if (isfinite(x)) {   // pandas rolling: +-inf -> NaN (Window._prep_values)
+            sm += x;
+            ++c;
+        }
+    }
+    out[((int64_t)p * nseg + ib) * kmax + k] = c >= minp ? sm / (double)c : NAN;
+    for (int i = ib + 1; i < ib + RPT && i < hi; ++i) {
+        const double xi = xs[(i - lo) * RKS + k];
+        if (isfinite(xi)) {
+            sm += xi;
+            ++c;
+        }
+        const int jo = i - window;   // leaves the window
+        if (jo >= 0) {
+            const double xo = xs[(jo - lo) * RKS + k];
+            if (isfinite(xo)) {
+                sm -= xo;
+                --c;
+            }
+        }
+        if (c == 0) sm = 0.0;
+        out[((int64_t)p * nseg + i) * kmax + k] = c >= minp ? sm / (double)c : NAN;
+    }
+}
+
+// Sixteen lanes per (problem, fitted-month row), sixteen rows per workgroup: lane a owns
+// regressor a (K <= 15), the quadratic forms c'Sxx c and c'Sxy are 16-lane sums.  Most rows
+// of a gathered series belong to other ranks' months and only write the zero record.
+constexpr int PG = 16;
+__global__ __launch_bounds__(TT) void predictive_kernel(const double* mom, int mom_stride,
+                                                        int nseg, int nprob,
+                                                        const int32_t* prob_k, const int32_t* idx,
+                                                        const int32_t* count, const double* roll,
+                                                        int pmax, int lag, int seg_lo, int seg_hi,
+                                                        double* pred, uint32_t* pst) {
+    const int p = blockIdx.y, lane = threadIdx.x % PG;
+    const int i = blockIdx.x * (TT / PG) + threadIdx.x / PG;
+    const bool row = i < nseg;
+    const int ic = row ? i : 0;
+    double* o = pred + ((int64_t)p * nseg + ic) * 4;
+    const int cnt = count[p];
+    const int s = ic < cnt ? idx[(int64_t)p * nseg + ic] : -1;
+    const bool other = ic < cnt && (s < seg_lo || s >= seg_hi);   // another rank's month
+    uint32_t st = 0;
+    double slope = NAN, r2 = NAN, nn = NAN;
+    const int K = prob_k[p];
+    const bool own = row && !other && ic < cnt && ic >= lag;
+    double tb = 0.0, ty = 0.0, syy = 0.0, n = 0.0;
+    bool bad = false;
+    if (own) {
+        const double* c = roll + ((int64_t)p * nseg + (ic - lag)) * pmax;
+        const double* mo = mom + ((int64_t)(s - seg_lo) * nprob + p) * mom_stride;
+        const int K1 = K + 1;
+        n = mo[0];
+        bad = lane <= K && isnan(c[lane]);
+        const double* S = mo + 1 + K1;
+        if (lane < K) {
+            double t = 0.0;
+            for (int b = 0; b < K; ++b) t += S[lane * K1 + b] * c[1 + b];
+            tb = c[1 + lane] * t;
+            ty = c[1 + lane] * S[lane * K1 + K];
+        }
+        syy = S[K * K1 + K];
+    }
+    // 16-lane sums / any (every lane of the group takes part)
+    int anybad = bad ? 1 : 0;
+#pragma unroll
+    for (int m = 8; m > 0; m >>= 1) {
+        tb += __shfl_xor(tb, m, PG);
+        ty += __shfl_xor(ty, m, PG);
+        anybad |= __shfl_xor(anybad, m, PG);
+    }
+    if (own && !anybad && n >= 2.0) {
+        slope = ty / tb;
+        r2 = (ty * ty) / (tb * syy);
+        nn = n;
+        st = FM_ST_FITTED;
+        if (!(tb > 0.0)) st |= FM_ST_CONST_COL;
+    }
+    if (row && lane == 0) {
+        if (other) {   // zero record for the sum-combine of sharded runs
+            o[0] = o[1] = o[2] = o[3] = 0.0;
+            pst[(int64_t)p * nseg + ic] = 0;
+        } else {
+            o[0] = slope;
+            o[1] = r2;
+            o[2] = nn;
+            o[3] = 0.0;
+            pst[(int64_t)p * nseg + ic] = st;
+        }
+    }
+}
+
+// Wide problems (> 16 coefficients) or windows > 257 rows: one workgroup per (problem,
+// coefficient, chunk of WRCH output rows), each output a direct sum over its window.
+constexpr int WRCH = 1024;
+
+__global__ __launch_bounds__(TT) void rolling_kernel_wide(const double* rec, int64_t r_seg,
+                                                     int64_t r_prob, const int32_t* idx,
+                                                     const int32_t* count, int nseg, int kmax,
+                                                     int window, int minp, double* out) {
+    __shared__ double xs[WRCH + RMAXW];
+    const int p = blockIdx.y / kmax, k = blockIdx.y - (blockIdx.y / kmax) * kmax;
+    const int c0 = blockIdx.x * WRCH;
+    const int cnt = count[p];
+    // rows past the fitted-month count have no month: NaN (never left uninitialised)
+    const int cend = c0 + WRCH < nseg ? c0 + WRCH : nseg;
     for (int i = (c0 > cnt ? c0 : cnt) + threadIdx.x; i < cend; i += TT)
         out[((int64_t)p * nseg + i) * kmax + k] = NAN;
     if (c0 >= cnt) return;
     const int32_t* ix = idx + (int64_t)p * nseg;
     const int lo = c0 - window + 1 < 0 ? 0 : c0 - window + 1;
-    const int hi = c0 + RCH < cnt ? c0 + RCH : cnt;
+    const int hi = c0 + WRCH < cnt ? c0 + WRCH : cnt;
     for (int j = lo + threadIdx.x; j < hi; j += TT)
         xs[j - lo] = rec[(int64_t)ix[j] * r_seg + (int64_t)p * r_prob + k];
     __syncthreads();
@@ -148,8 +474,9 @@ __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t 
     }
 }
 
-// One wave per (problem, fitted-month row); lane a owns regressor a.
-__global__ __launch_bounds__(WAVE) void predictive_kernel(const double* mom, int mom_stride,
+// Wide problems (> 15 regressors): one wave per (problem, fitted-month row), lane a owns
+// regressor a.
+__global__ __launch_bounds__(WAVE) void predictive_kernel_wide(const double* mom, int mom_stride,
                                                           int nseg, int nprob,
                                                           const int32_t* prob_k, const int32_t* idx,
                                                           const int32_t* count, const double* roll,
@@ -238,8 +565,8 @@ extern "C" int fm_ts_compact(const uint32_t* status, int64_t s_seg, int64_t s_pr
     using namespace fm;
     FM_REQUIRE(status && idx && count, "fm_ts_compact: null pointer");
     if (nprob == 0) return FM_OK;
-    hipLaunchKernelGGL(compact_kernel, dim3(nprob), dim3(TT), 0, (hipStream_t)stream, status, s_seg,
-                       s_prob, nseg, idx, count);
+    hipLaunchKernelGGL(compact_kernel, dim3((nseg + CB - 1) / CB > 0 ? (nseg + CB - 1) / CB : 1, nprob), dim3(TT), 0,
+                       (hipStream_t)stream, status, s_seg, s_prob, nseg, idx, count);
     FM_CHECK_LAUNCH("fm_ts_compact");
     return FM_OK;
 }
@@ -253,8 +580,16 @@ extern "C" int fm_ts_summary(const double* rec, int64_t r_seg, int64_t r_prob, c
                "fm_ts_summary: null pointer");
     FM_REQUIRE(nw_lags >= 0, "fm_ts_summary: nw_lags < 0");
     if (nprob == 0 || kmax == 0) return FM_OK;
-    SumArgs a{rec, r_seg, r_prob, idx, count, nseg, kmax, nw_lags, mean, se, tstat, nobs, work};
-    hipLaunchKernelGGL(summary_kernel, dim3(kmax, nprob), dim3(TT), 0, (hipStream_t)stream, a);
+    SumArgs a{rec, r_seg, r_prob, idx, count, nseg, kmax, nw_lags, nprob, mean, se, tstat, nobs, work};
+    const int nchunk = (nseg + SCH - 1) / SCH;
+    if (nseg >= SUM_CHUNKED && nw_lags <= SUM_MAXLAG) {
+        hipStream_t st = (hipStream_t)stream;
+        hipLaunchKernelGGL(summary_gather_kernel, dim3((nseg + GROWS - 1) / GROWS, nprob), dim3(TT), 0, st, a);
+        hipLaunchKernelGGL(summary_part_kernel, dim3(nchunk, kmax, nprob), dim3(TT), 0, st, a);
+        hipLaunchKernelGGL(summary_combine_kernel, dim3(kmax, nprob), dim3(WAVE), 0, st, a, nchunk);
+    } else {
+        hipLaunchKernelGGL(summary_kernel, dim3(kmax, nprob), dim3(TT), 0, (hipStream_t)stream, a);
+    }
     FM_CHECK_LAUNCH("fm_ts_summary");
     return FM_OK;
 }
@@ -268,9 +603,15 @@ extern "C" int fm_rolling_mean(const double* rec, int64_t r_seg, int64_t r_prob,
     FM_REQUIRE(window >= 1 && window <= RMAXW && min_periods >= 0,
                "fm_rolling_mean: window must be 1..%d", RMAXW);
     if (nprob == 0 || nseg == 0 || kmax == 0) return FM_OK;
-    dim3 grid((nseg + RCH - 1) / RCH, nprob * kmax);
-    hipLaunchKernelGGL(rolling_kernel, grid, dim3(TT), 0, (hipStream_t)stream, rec, r_seg, r_prob,
-                       idx, count, nseg, kmax, window, min_periods, out);
+    if (kmax <= RKMAX && window <= RSPAN - RCH + 1) {
+        dim3 grid((nseg + RCH - 1) / RCH, nprob);
+        hipLaunchKernelGGL(rolling_kernel, grid, dim3(TT), 0, (hipStream_t)stream, rec, r_seg, r_prob,
+                           idx, count, nseg, kmax, window, min_periods, out);
+    } else {
+        dim3 grid((nseg + WRCH - 1) / WRCH, nprob * kmax);
+        hipLaunchKernelGGL(rolling_kernel_wide, grid, dim3(TT), 0, (hipStream_t)stream, rec, r_seg, r_prob,
+                           idx, count, nseg, kmax, window, min_periods, out);
+    }
     FM_CHECK_LAUNCH("fm_rolling_mean");
     return FM_OK;
 }
@@ -285,10 +626,16 @@ extern "C" int fm_predictive(const double* moments, int32_t mom_stride, int32_t 
                "fm_predictive: null pointer");
     FM_REQUIRE(lag >= 1, "fm_predictive: lag must be >= 1");
     if (nprob == 0 || nseg == 0) return FM_OK;
-    dim3 grid(nseg, nprob);
-    hipLaunchKernelGGL(predictive_kernel, grid, dim3(WAVE), 0, (hipStream_t)stream, moments,
-                       mom_stride, nseg, nprob, prob_k, idx, count, rolling, pmax, lag, seg_lo,
-                       seg_hi, pred, pred_status);
+    if (pmax <= PG) {
+        dim3 grid((nseg + TT / PG - 1) / (TT / PG), nprob);
+        hipLaunchKernelGGL(predictive_kernel, grid, dim3(TT), 0, (hipStream_t)stream, moments,
+                           mom_stride, nseg, nprob, prob_k, idx, count, rolling, pmax, lag, seg_lo,
+                           seg_hi, pred, pred_status);
+    } else {
+        hipLaunchKernelGGL(predictive_kernel_wide, dim3(nseg, nprob), dim3(WAVE), 0, (hipStream_t)stream, moments,
+                           mom_stride, nseg, nprob, prob_k, idx, count, rolling, pmax, lag, seg_lo,
+                           seg_hi, pred, pred_status);
+    }
     FM_CHECK_LAUNCH("fm_predictive");
     return FM_OK;
 }

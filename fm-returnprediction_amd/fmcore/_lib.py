@@ -50,7 +50,7 @@ class SelectArgs(C.Structure):
         ("cols", _p), ("col_stride", _i64), ("ncols", _i32), ("seg_off", _p), ("nseg", _i32),
         ("max_seg_len", _i32), ("row_mask", _p), ("q_lo", _f64), ("q_hi", _f64),
         ("min_count", _i32), ("lerp_mode", _i32), ("lo", _p), ("hi", _p), ("nvalid", _p),
-        ("mean", _p), ("sd", _p), ("center", _p),
+        ("mean", _p), ("sd", _p), ("center", _p), ("level", _p),
     ]
 
 

@@ -216,9 +216,10 @@ class Cuts:
 
 
 def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols=None,
-                row_mask=None, moments=False, center=False, tag="fm_select_cuts"):
+                row_mask=None, moments=False, center=False, level=None, tag="fm_select_cuts"):
     """Per (column, month) quantile cuts.  ``cols`` defaults to panel.cols.  ``moments``:
-    also the clipped mean / sd; ``center``: also a Gram pivot inside the data (fm_select)."""
+    also the clipped mean / sd; ``center``: also a Gram pivot inside the data; ``level``
+    (uint8 [rows], one column): every row's (x >= lo) + (x >= hi) (fm_select)."""
     src = panel.cols if cols is None else cols
     if src.dim() == 1:
         src = src.view(1, -1)
@@ -236,9 +237,10 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
     sa = L.SelectArgs(cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, seg_off=panel.seg_off.data_ptr(),
                       nseg=T, max_seg_len=max(panel.max_seg_len, 1), row_mask=_ptr(row_mask), q_lo=float(q_lo),
                       q_hi=float(q_hi), min_count=int(min_count), lerp_mode=int(mode), lo=lo.data_ptr(),
-                      hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=_ptr(mean), sd=_ptr(sd), center=_ptr(cen))
+                      hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=_ptr(mean), sd=_ptr(sd), center=_ptr(cen),
+                      level=_ptr(level))
     _kcall(tag, "fm_select", L.C.byref(sa), _stream())
-    _remember(tag, "fm_select", sa, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off)
+    _remember(tag, "fm_select", sa, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, level)
     return Cuts(lo, hi, nv, mean, sd, cen)
 
 
@@ -259,10 +261,11 @@ def standardize(panel: DevicePanel, mean, sd, src=None, out=None):
     return out
 
 
-def nyse_breakpoints(panel: DevicePanel, q_a=0.2, q_b=0.5):
-    """me_20 / me_50 per month over NYSE rows (pandas groupby.quantile lerp)."""
+def nyse_breakpoints(panel: DevicePanel, q_a=0.2, q_b=0.5, level=None):
+    """me_20 / me_50 per month over NYSE rows (pandas groupby.quantile lerp); with ``level``
+    (uint8 [rows]) also every row's universe level from them, in the same call."""
     cuts = select_cuts(panel, q_a, q_b, 1, LERP_PANDAS, cols=panel.me.view(1, -1), row_mask=panel.nyse,
-                       tag="fm_select_cuts[nyse]")
+                       level=level, tag="fm_select_cuts[nyse]")
     return cuts.lo[0], cuts.hi[0]
 
 
@@ -276,11 +279,12 @@ def universe_level(panel: DevicePanel, cut_a, cut_b):
 def universe(panel: DevicePanel, q_a=0.2, q_b=0.5):
     """get_subsets on the device (reference src/calc_Lewellen_2014.py:69-105): the NYSE
     me_20 / me_50 breakpoints and the nested universe level byte of every row, one launch
-    (fm_universe); months longer than its register budget take fm_select_cuts (row mask)
-    + fm_universe_level.  Returns (cut_a [T], cut_b [T], level [rows] uint8)."""
+    (fm_universe); months longer than its register budget take fm_select (row mask, the
+    level bytes written by the same call).  Returns (cut_a [T], cut_b [T], level [rows] uint8)."""
     if panel.max_seg_len > UNIVERSE_MAX_ROWS:
-        a, b = nyse_breakpoints(panel, q_a, q_b)
-        return a, b, universe_level(panel, a, b)
+        level = torch.empty(panel.nrows, dtype=torch.uint8, device=panel.cols.device)
+        a, b = nyse_breakpoints(panel, q_a, q_b, level=level)
+        return a, b, level
     dev = panel.cols.device
     a = torch.empty(panel.nseg, dtype=torch.float64, device=dev)
     b = torch.empty_like(a)
@@ -635,7 +639,8 @@ def ts_summary(rec, r_seg, r_prob, ix: TSIndex, nseg, nprob, kmax, nw_lags=4):
     mean = torch.empty((nprob, kmax), dtype=torch.float64, device=dev)
     se, ts = torch.empty_like(mean), torch.empty_like(mean)
     nobs = torch.empty((nprob, kmax), dtype=torch.int32, device=dev)
-    work = torch.empty((nprob, kmax, max(nseg, 1)), dtype=torch.float64, device=dev)
+    # the series [nprob][kmax][nseg] and the long-series chunk partials (fm_hip.h)
+    work = torch.empty(nprob * kmax * (max(nseg, 1) + -(-nseg // 2048) * 28), dtype=torch.float64, device=dev)
     _kcall("fm_ts_summary", "fm_ts_summary", rec.data_ptr(), r_seg, r_prob, ix.idx.data_ptr(), ix.count.data_ptr(),
            nseg, nprob, kmax, nw_lags, mean.data_ptr(), se.data_ptr(), ts.data_ptr(), nobs.data_ptr(),
            work.data_ptr(), _stream())

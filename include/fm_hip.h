@@ -158,7 +158,8 @@ int fm_select_cuts(const double* cols, int64_t col_stride, int32_t ncols,
  * Outputs are [ncols][nseg]; every output pointer except lo / hi may be NULL.
  *   mean, sd: moments of the clipped values (ddof = 1), for the per-month standardization;
  *   center:   a pivot inside the data for the Gram (midpoint of the cuts, else of the
- *             segment's finite range, else 0); costs nothing beyond the cuts.
+ *             segment's finite range, else 0); costs nothing beyond the cuts;
+ *   level:    the universe level byte of every row from the two cuts (see the field).
  * Without a row mask and for segments of <= 6144 rows, passing nvalid enables the
  * one-wave-per-(segment, column) fast path (nvalid carries its fallback marks). */
 typedef struct fm_select_args {
@@ -178,6 +179,11 @@ typedef struct fm_select_args {
     double* mean;
     double* sd;
     double* center;
+    uint8_t* level;              /* [rows] or NULL; ncols == 1 only: every row's universe level
+                                    (x >= lo) + (x >= hi) of the UNMASKED column (NaN compares
+                                    False), i.e. get_subsets' nested masks from the NYSE cuts
+                                    (src/calc_Lewellen_2014.py:95-105), by a streaming
+                                    launch after the cuts (same stream) */
 } fm_select_args;
 
 int fm_select(const fm_select_args* args, void* stream);
@@ -234,6 +240,8 @@ int fm_solve_fixup(const double* cols, int64_t col_stride, const int64_t* seg_of
 int fm_ts_compact(const uint32_t* status, int64_t s_seg, int64_t s_prob, int32_t nseg,
                   int32_t nprob, int32_t* idx, int32_t* count, void* stream);
 
+/* fm_ts_summary: work holds nprob * kmax * (nseg + ceil(nseg / 2048) * 28) doubles (series of
+ * >= 4096 months take the chunked one-pass kernels, whose partials follow the series). */
 int fm_ts_summary(const double* rec, int64_t r_seg, int64_t r_prob, const int32_t* idx,
                   const int32_t* count, int32_t nseg, int32_t nprob, int32_t kmax,
                   int32_t nw_lags, double* mean, double* se, double* tstat, int32_t* nobs,

@@ -241,6 +241,40 @@ def test_masked_middle_quantiles_hist_select(E):
         assert _same([b[t]], [O.pandas_quantile(x[m], 0.5)]), t
 
 
+@pytest.mark.parametrize("maxlen", [6000, 20000, 30000])
+def test_select_level_output(E, maxlen):
+    """fm_select's level output (get_subsets' nested masks from the NYSE cuts, reference
+    src/calc_Lewellen_2014.py:95-105) after every select path: <= 6,144-row months (the
+    workgroup kernel), 6,145..20,480 (the register kernel), longer (streaming); NaN me on
+    NYSE and other rows, a month without NYSE rows (NaN cuts: level 0)."""
+    import torch
+    rng = np.random.default_rng(maxlen)
+    segs, masks = [], []
+    for n in (1, 7, 300, maxlen // 2, maxlen):
+        x = np.exp(rng.normal(5, 2, n))
+        x[rng.random(n) < 0.05] = np.nan
+        segs.append(x)
+        masks.append(rng.random(n) < 0.4)
+    segs.append(np.exp(rng.normal(5, 2, 500)))
+    masks.append(np.zeros(500, dtype=bool))
+    vals = np.concatenate(segs)
+    mask = np.concatenate(masks).astype(np.uint8)
+    labels = np.repeat(np.arange(len(segs)), [len(x) for x in segs])
+    panel = E.panel_from_arrays([vals], ["me"], labels, me=vals, nyse=mask)
+    level = torch.full((panel.nrows,), 7, dtype=torch.uint8, device=panel.cols.device)
+    a, b = E.nyse_breakpoints(panel, level=level)
+    a, b, level = a.cpu().numpy(), b.cpu().numpy(), level.cpu().numpy()
+    off = panel.seg_off_h
+    for t, (x, m) in enumerate(zip(segs, masks)):
+        v = x[m & ~np.isnan(x)]
+        ea = O.pandas_quantile(v, 0.2) if v.size else np.nan
+        eb = O.pandas_quantile(v, 0.5) if v.size else np.nan
+        assert _same([a[t]], [ea]) and _same([b[t]], [eb]), t
+        with np.errstate(invalid="ignore"):
+            exp = (x >= ea).astype(np.uint8) + (x >= eb).astype(np.uint8)
+        assert np.array_equal(level[off[t]:off[t + 1]], exp), t
+
+
 def test_universe_kernel_vs_oracle(E):
     """fm_universe (NYSE me_20 / me_50 + the nested level byte, one launch) against the
     pandas lerp restatement and the reference's masks (me >= cut, NaN False): months of
@@ -480,6 +514,46 @@ def test_newey_west_golden(R):
     for case in load_json("nw.json"):
         got = R.newey_west_mean_se(np.array(case["x"]), case["lags"])
         assert scalar_close(got, case["se"], 1e-12), case["lags"]
+
+
+@pytest.mark.parametrize("T", [4095, 4096, 10000, 100000])
+def test_long_series_summary_vs_oracle(E, T):
+    """fm_ts_summary on long series (>= 4,096 months: the chunked one-pass kernels -- shifted
+    sums and lagged cross sums per 2,048-row chunk, combined in chunk order) against the
+    oracle's two-pass mean / Newey-West s.e. on the dropna'd series, lags 0..8: NaN runs
+    across chunk boundaries (longer than the lag), a NaN-led series, a series with a large
+    mean relative to its spread, an all-NaN column and a column with one value."""
+    import torch
+    from fmcore import api
+    rng = np.random.default_rng(T)
+    cols = []
+    x = rng.standard_normal(T) * 0.05 + 0.01
+    x[rng.random(T) < 0.1] = np.nan
+    x[2040:2060] = np.nan                      # straddles the first chunk boundary
+    cols.append(x)
+    y = rng.standard_t(3, T)
+    y[:7] = np.nan                             # K0 is the 8th value
+    cols.append(y)
+    cols.append(1e3 + rng.standard_normal(T) * 1e-3)   # mean >> spread
+    cols.append(np.full(T, np.nan))
+    z = np.full(T, np.nan)
+    z[T // 2] = 2.5
+    cols.append(z)
+    vals = torch.from_numpy(np.stack(cols, axis=1)).to(E.require_device())
+    for lags in (0, 1, 4, 8):
+        mean, se, t, nobs = api.records_summary_device(vals, lags)
+        for j, c in enumerate(cols):
+            v = c[~np.isnan(c)]
+            assert nobs[j] == v.size, (lags, j)
+            if v.size == 0:
+                assert np.isnan(mean[j]) and np.isnan(se[j])
+                continue
+            assert scalar_close(mean[j], v.mean(), RTOL, 1e-12), (lags, j)
+            exp = O.newey_west_mean_se(v, lags)
+            if np.isnan(exp):
+                assert np.isnan(se[j]), (lags, j)
+            else:
+                assert scalar_close(se[j], exp, 1e-9, 1e-15), (lags, j, se[j], exp)
 
 
 @pytest.mark.parametrize("fixture,panel", [("fig1.npz", cases.fig1_panel), ("fig1c.npz", cases.fig1_const_panel)])

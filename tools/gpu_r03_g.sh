@@ -1,0 +1,7 @@
+# Round-3 iteration g: long-series ts kernels v2 + fm_select level output
+T="python -u -m pytest -x -q -p no:cacheprovider --timeout 200 --timeout-method thread"
+tools/gpu_steps.sh \
+ "tstests:::400:::$T tests/test_gpu_parity.py -k 'long_series or per_stage or unfitted or gathered or c5 or headline or newey or level_output or masked or universe or forecast_api'" \
+ "gputests:::600:::$T tests -m gpu" \
+ "bench:::400:::python bench.py --steps 20" \
+ "kstats:::400:::cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/kt -o kt --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-chars --steps 10"
