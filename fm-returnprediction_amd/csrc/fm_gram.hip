@@ -23,7 +23,10 @@ namespace {
 
 constexpr int GT = 256;
 constexpr int GNW = GT / WAVE;
-constexpr int GRAM_MINW = FM_GRAM_PF2 ? 2 : 3;   // waves per SIMD the register budget allows
+#ifndef FM_GRAM_MINW
+#define FM_GRAM_MINW (FM_GRAM_PF2 ? 2 : 3)
+#endif
+constexpr int GRAM_MINW = FM_GRAM_MINW;   // waves per SIMD the register budget allows
 
 // One workgroup per chunk (normally a whole month: the chunk plan makes chunks as large as
 // the chip's resident workgroup slots allow, so the prologue and the cross-wave epilogue run
