@@ -201,8 +201,8 @@ __global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
 //     c(tau) >= k+1.  The candidates -- every value whose high word is <= tau -- are then a
 //     PREFIX of the sorted values holding at least k+1 of them, so the order statistics are
 //     ranks inside the candidates (the upper tail the same on complemented keys);
-//   * both tails' candidates (a little more than 2k values) are compacted to LDS with one
-//     block scan; each wave sorts one 64-key run of each tail and every candidate finds its
+//   * both tails' candidates (a little more than 2k values) are compacted to LDS (ballot
+//     counts per wave, one barrier for the wave offsets); each wave sorts one 64-key run of each tail and every candidate finds its
 //     merged rank by binary searches in the other runs, so the whole workgroup works on the
 //     order statistics (no single-wave sort of hundreds of keys).
 // Units it cannot finish (ranks >= 512, > 512 candidates per tail, too few valid thread
@@ -219,6 +219,7 @@ struct LongSmem {
     SelSmemT<LNW> hs;            // hist_select scratch (and the block reductions)
     uint32_t tw[2][LNW];         // per-wave thresholds T_w (high words)
     int tot[2][LNW];             // c(T_w), summed over the waves
+    int wc[2][LNW];              // per-wave candidate counts
     uint64_t res[4];             // keys of the four order statistics
 };
 
@@ -346,23 +347,44 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
             const uint64_t kub = ~(((uint64_t)tu << 32) | 0xFFFFFFFFull);
             const double tlo = kla >= dkey(INFINITY) ? INFINITY : kval(kla);
             const double thi = kub <= dkey(-INFINITY) ? -INFINITY : kval(kub);
-            int cc = 0;
+            // wave totals from ballots (compares straight into lane masks, scalar counts),
+            // then each wave's offset from the other waves' totals (one barrier)
+            int wl = 0, wh = 0;
 #pragma unroll
-            for (int v = 0; v < VPT; ++v) cc += (xv[v] <= tlo ? 1 : 0) + (xv[v] >= thi ? 0x10000 : 0);
-            int tot = 0;
-            const int off = block_excl_scan<LNW>(cc, sm.hs.ints, &tot);
-            clo = tot & 0xFFFF;
-            chi = tot >> 16;
+            for (int v = 0; v < VPT; ++v) {
+                wl += (int)__popcll(__ballot(xv[v] <= tlo));
+                wh += (int)__popcll(__ballot(xv[v] >= thi));
+            }
+            if (lane == 0) {
+                sm.wc[0][w] = wl;
+                sm.wc[1][w] = wh;
+            }
+            __syncthreads();
+            int ol = 0, oh = LCAP;
+#pragma unroll
+            for (int q = 0; q < LNW; ++q) {
+                const int a0 = sm.wc[0][q], a1 = sm.wc[1][q];
+                ol += q < w ? a0 : 0;
+                oh += q < w ? a1 : 0;
+                clo += a0;
+                chi += a1;
+            }
             // caps, and the rare overlap of the two sets (massive ties): redone by the fallback
             ok = clo <= LCAP && chi <= LCAP && clo + chi <= n && clo > kl && chi > ku;
             if (ok) {
-                int ol = off & 0xFFFF, oh = LCAP + (off >> 16);
 #pragma unroll
                 for (int v = 0; v < VPT; ++v) {
                     double x = xv[v];
                     asm volatile("" : "+v"(x));   // recompute (no SGPR masks kept from the count)
-                    if (x <= tlo) sm.cand[ol++] = x;
-                    if (x >= thi) sm.cand[oh++] = x;
+                    const uint64_t ml = __ballot(x <= tlo), mh = __ballot(x >= thi);
+                    if (ml) {   // wave-uniform: most value slots hold no candidate
+                        if (x <= tlo) sm.cand[ol + mask_rank(ml)] = x;
+                        ol += (int)__popcll(ml);
+                    }
+                    if (mh) {
+                        if (x >= thi) sm.cand[oh + mask_rank(mh)] = x;
+                        oh += (int)__popcll(mh);
+                    }
                 }
                 __syncthreads();
                 // the four order statistics among the candidates: wave w sorts run w of each

@@ -34,6 +34,9 @@ constexpr double EIG_REL = 1e-12;
 // the 1e-9 contract, so the problem is flagged FM_ST_REFIT and re-solved from its rows by
 // fm_solve_fixup (Householder QR + SVD of R: error ~eps * cond(X), as statsmodels' SVD).
 constexpr double REFIT_REL = 1e-6;
+#ifndef FM_AB_SOLVE_STOP
+#define FM_AB_SOLVE_STOP 0    // timing builds only: 1 stop after the bucket sums, 2 after the centering
+#endif
 #ifndef FM_AB_SOLVE_NOMOM
 #define FM_AB_SOLVE_NOMOM 0   // timing builds only (tools/build_variant.sh): skip the moments store
 #endif
@@ -452,6 +455,10 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         }
     }
     __syncthreads();
+    if (FM_AB_SOLVE_STOP == 1) {
+        if (tid == 0) a.status[(int64_t)s * a.nprob] = (uint32_t)bs[0];
+        return;
+    }
     const int g = lane >> 4, i = lane & 15;
     const int rs = a.pmax + 2;
     double* T = wsc[w] + g * TT;
@@ -535,6 +542,10 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         }
         if (act0 && (t_flags[pp] & 1) != 0) {
             if ((__ballot(i >= 1 && i <= K && !(sii > 1e-10 * gdiag)) & gm) != 0) st |= FM_ST_CONST_SUSPECT;
+        }
+        if (FM_AB_SOLVE_STOP == 2) {
+            if (live && i == 0) a.rec[ro] = row[0] + row[1] + mu;
+            continue;
         }
         // ---- augmented Cholesky of S (pivot r = k sits in lane k + 1)
         bool ok = act0, illc = false;

@@ -12,7 +12,10 @@
  *                      groupby("mthcaldt")["me"].quantile([.2,.5]) over NYSE rows (:74-82)
  *   fm_select       <- the same, struct-argument form: wave-per-(month, column) tail
  *                      selection with an exact workgroup fallback, plus the Gram pivot
- *                      `center` (the Table-2 fast path; fm_select_cuts calls it)
+ *                      `center` (the Table-2 fast path; fm_select_cuts calls it); months
+ *                      of 6,145 .. 20,480 rows (C5) one register-resident 512-thread
+ *                      workgroup per (month, column), longer ones streamed; optionally the
+ *                      universe level bytes from the cuts (get_subsets :95-105)
  *   fm_clip         <- subdf[var].clip(lower, upper) (src/calc_Lewellen_2014.py:524)
  *   fm_standardize  <- per-month z-score (north-star extension; no reference line)
  *   fm_universe_level <- me >= me_20 / me >= me_50 masks (src/calc_Lewellen_2014.py:95-96)
