@@ -209,6 +209,9 @@ __global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
 // minima) are marked (nvalid = -1) and redone by the streaming kernel's fallback pass.  At
 // <= 128 VGPRs (4 waves per SIMD) two workgroups share a CU, so one unit's loads fly while
 // the other selects.
+#ifndef FM_AB_LONG_MASKALL
+#define FM_AB_LONG_MASKALL 0   // timing builds only: mask every value slot
+#endif
 constexpr int LT = 512;
 constexpr int LNW = LT / WAVE;
 constexpr int LONG_VPT = 40;
@@ -242,11 +245,21 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
     double xv[VPT];
     if (!MID || a.mask == nullptr) {   // block-uniform
 #pragma unroll
-        for (int v = 0; v < VPT; ++v) {   // unconditional (clamped) loads, masked after
+        for (int v = 0; v < VPT; ++v) {   // unconditional (clamped) loads
             const uint32_t off = lb + (uint32_t)(v * LT * 8);
-            const double x = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
-            xv[v] = off <= lastb && L > 0 ? x : NAN;
+            xv[v] = *(const __attribute__((address_space(1))) double*)(src + (off < lastb ? off : lastb));
         }
+        // masked after, and only the slots past the block's full rows of values (a scalar
+        // branch per slot; the volatile asm keeps it a branch, not three selects per value)
+        const int vf = FM_AB_LONG_MASKALL ? 0 : L / LT;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v)
+            if (v >= vf) {
+                const uint32_t off = lb + (uint32_t)(v * LT * 8);
+                double x = xv[v];
+                asm volatile("" : "+v"(x));
+                xv[v] = off <= lastb && L > 0 ? x : NAN;
+            }
     } else {
         const gptr mb = (gptr)(a.mask + r0);
 #pragma unroll
@@ -396,15 +409,16 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
                 const int e = w * WAVE + lane;
                 uint64_t ka[1] = {e < clo ? dkey(sm.cand[e]) : SENT};
                 uint64_t kb[1] = {e < chi ? ~dkey(sm.cand[LCAP + e]) : SENT};
-                if (FM_AB_LONG != 2) {
-                    wave_sort<1>(ka);
-                    wave_sort<1>(kb);
-                }
+                const int nrl = __builtin_amdgcn_readfirstlane((clo + WAVE - 1) / WAVE);
+                const int nru = __builtin_amdgcn_readfirstlane((chi + WAVE - 1) / WAVE);
+                // only the waves holding candidates sort (an all-sentinel run is sorted);
+                // block-uniform counts, so the sorts run with the whole wave active
+                if (FM_AB_LONG != 2 && w < nrl) wave_sort<1>(ka);
+                if (FM_AB_LONG != 2 && w < nru) wave_sort<1>(kb);
                 ck[e] = ka[0];   // in place: wave w owns entries [64 w, 64 w + 64) of each list
                 ck[LCAP + e] = kb[0];
                 if (tid < 4) sm.res[tid] = SENT;
                 __syncthreads();
-                const int nrl = (clo + WAVE - 1) / WAVE, nru = (chi + WAVE - 1) / WAVE;
                 if (ka[0] != SENT) {
                     int r = lane;
                     for (int u = 0; u < nrl; ++u)

@@ -37,6 +37,9 @@ constexpr double REFIT_REL = 1e-6;
 #ifndef FM_AB_SOLVE_STOP
 #define FM_AB_SOLVE_STOP 0    // timing builds only: 1 stop after the bucket sums, 2 after the centering
 #endif
+#ifndef FM_AB_SOLVE_MOMROW
+#define FM_AB_SOLVE_MOMROW 0  // timing builds only: the moments stored one S row per lane
+#endif
 #ifndef FM_AB_SOLVE_NOMOM
 #define FM_AB_SOLVE_NOMOM 0   // timing builds only (tools/build_variant.sh): skip the moments store
 #endif
@@ -535,9 +538,16 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
             if (i == 0) mo[0] = n;
             if (srow) {
                 mo[i] = mu;   // mo[1 + r]
+                // S is exactly symmetric (S[r][c] and S[c][r] are the same products of the
+                // same packed sums), so lane r stores column r of S: S[c][r] for every c, and
+                // each store instruction writes K1 consecutive doubles (a row-per-lane store
+                // strides K1 doubles between lanes)
 #pragma unroll
                 for (int c = 0; c < G16 - 1; ++c)
-                    if (c < K1) mo[1 + K1 + (i - 1) * K1 + c] = row[c];
+                    if (c < K1) {
+                        if (FM_AB_SOLVE_MOMROW) mo[1 + K1 + (i - 1) * K1 + c] = row[c];
+                        else mo[1 + K1 + c * K1 + (i - 1)] = row[c];
+                    }
             }
         }
         if (act0 && (t_flags[pp] & 1) != 0) {
