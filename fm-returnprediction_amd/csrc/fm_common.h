@@ -61,18 +61,19 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 // Value of lane (this lane ^ J), without LDS: DPP quad_perm (1, 2), two bank-masked DPP
 // row rotations (4), DPP row_ror:8 (8), v_permlane16_swap / v_permlane32_swap (16, 32).
-// Verified against __shfl_xor by tools/probes/xor_probe.hip.
+// Verified against __shfl_xor by tools/probes/xor_probe.hip.  Where every lane has a source
+// lane (J = 1, 2, 8) mov_dpp is used: it has no "old" operand, so no copy of x is made first.
 template <int J>
 __device__ __forceinline__ uint32_t xor_lanes(uint32_t x) {
     if constexpr (J == 1) {
-        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0xB1, 0xF, 0xF, false);
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
     } else if constexpr (J == 2) {
-        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x4E, 0xF, 0xF, false);
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);
     } else if constexpr (J == 4) {
         const int t = __builtin_amdgcn_update_dpp((int)x, (int)x, 0x12C, 0xF, 0x5, false);   // lanes 0-3, 8-11
         return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)x, 0x124, 0xF, 0xA, false);    // lanes 4-7, 12-15
     } else if constexpr (J == 8) {
-        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xF, 0xF, false);
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, true);
     } else if constexpr (J == 16) {
         const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
         return (__lane_id() & 16) ? r[0] : r[1];

@@ -29,6 +29,9 @@
 #ifndef FM_AB_GRAM_NOSCATTER
 #define FM_AB_GRAM_NOSCATTER 0
 #endif
+#ifndef FM_AB_GRAM_DPPOLD
+#define FM_AB_GRAM_DPPOLD 0   // 1: the rotations through update_dpp(0, ...) (zero-initialised)
+#endif
 #ifndef FM_GRAM_PF2
 #define FM_GRAM_PF2 0   // 1: two tiles of row loads in flight per wave (two register buffers)
 #endif
@@ -44,11 +47,18 @@ __device__ __forceinline__ uint32_t push_valid(uint32_t nn, double x) {
 
 // Lane value rotated within each 16-lane row: DPP row_ror:N gives lane i the value of lane
 // (i - N) & 15 of its row (fm_common.h xor_lanes<4> relies on the same rule).
+// Every lane of a rotation has a source lane, so the DPP "old" value is never used: mov_dpp
+// (no old operand) spares the two zero-initialising moves update_dpp(0, ...) costs per half.
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double x) {
     const uint64_t u = (uint64_t)__double_as_longlong(x);
+#if FM_AB_GRAM_DPPOLD
     const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+#else
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+#endif
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 

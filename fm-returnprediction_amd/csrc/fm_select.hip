@@ -209,6 +209,9 @@ __global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
 // minima) are marked (nvalid = -1) and redone by the streaming kernel's fallback pass.  At
 // <= 128 VGPRs (4 waves per SIMD) two workgroups share a CU, so one unit's loads fly while
 // the other selects.
+#ifndef FM_AB_PAIR_MASKALL
+#define FM_AB_PAIR_MASKALL 0   // timing builds only: test every value slot against the end
+#endif
 #ifndef FM_AB_LONG_MASKALL
 #define FM_AB_LONG_MASKALL 0   // timing builds only: mask every value slot
 #endif
@@ -691,9 +694,16 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
         // ---- 1. this wave's half: count, lane extrema (NaN = absent / masked out)
         int nh = 0;
         double mn4[4] = {NAN, NAN, NAN, NAN}, mx4[4] = {NAN, NAN, NAN, NAN};
+        // slots past the segment end -> NaN; only the slots past the unit's full 128-row
+        // groups can hold such rows (a scalar branch per slot, kept a branch by the asm)
+        const int vf = FM_AB_PAIR_MASKALL ? 0 : L / (2 * WAVE);
 #pragma unroll
         for (int v = 0; v < VPH; ++v) {
-            if (row0 + v * 2 * WAVE >= L) xv[v] = NAN;   // past the segment end
+            if (v >= vf) {
+                double x = xv[v];
+                asm volatile("" : "+v"(x));
+                xv[v] = row0 + v * 2 * WAVE >= L ? (double)NAN : x;
+            }
             const double x = xv[v];
             nh += (int)__popcll(__ballot(!isnan(x)));
             mn4[v & 3] = hw_min(mn4[v & 3], x);

@@ -380,7 +380,8 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
 
 template <int L>
 __device__ __forceinline__ int rowbc_i(int v) {   // lane L of this lane's 16-lane row
-    return __builtin_amdgcn_update_dpp(0, v, 0x150 + L, 0xF, 0xF, false);
+    // every lane has a source (row_newbcast): mov_dpp needs no zero-initialised destination
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, true);
 }
 template <int L>
 __device__ __forceinline__ double rowbc(double v) {
