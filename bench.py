@@ -1,14 +1,24 @@
 """Benchmark: the full Fama-MacBeth pass (BASELINE.json metric) on MI355X.
 
-Workload per GPU (BASELINE configs C3+C4): a 600-month x 5,000-firm synthetic panel with
-15 characteristics (retx + the 14 Lewellen predictors), generated in HBM by fm_gen_panel.
-One step = winsorize all 15 columns (1/99) -> NYSE me breakpoints + nested universes ->
-Models 1/2/3 x {All, All-but-tiny, Large} + the Figure-1 model x {All, Large} (11
-cross-sectional problems per month) in one batched Gram pass -> solves -> all-gather of
-the monthly records -> Fama-MacBeth means + Newey-West(4) -> 120/60 rolling means ->
-lagged-rolling forecasts + predictive-slope FM summaries.  Inputs are HBM-resident when
-the timed region starts.  With N GPUs (torchrun) each rank owns 600 months of a 600*N-month
-panel (weak scaling); value = all ranks' firm-month rows / max-over-ranks time.
+Workloads (one step = one pass of the hot path over the rank's months, inputs HBM-resident):
+
+* headline (default at N=1; BASELINE configs C3+C4): a 600-month x 5,000-firm synthetic
+  panel with 15 characteristics (retx + the 14 Lewellen predictors), generated in HBM by
+  fm_gen_panel.  One step = winsorize all 15 columns (1/99) -> NYSE me breakpoints + nested
+  universes -> Models 1/2/3 x {All, All-but-tiny, Large} + the Figure-1 model x {All, Large}
+  (11 cross-sectional problems per month) in one batched Gram pass -> solves -> Fama-MacBeth
+  means + Newey-West(4) -> 120/60 rolling means -> lagged-rolling forecasts +
+  predictive-slope FM summaries.
+* c5 (default at N>1; BASELINE configs[4]): every rank owns 12,500 months x 20,000 firms x 15
+  characteristics of a 12,500*N-month panel (at N=8 exactly C5's 100,000 x 20,000 x 15), the
+  same pass through fmcore.step.ShardedStep: local pass -> RCCL all-gather of the monthly
+  records -> time-series stage on the gathered series -> RCCL SUM all-reduce of the
+  predictive records -> predictive summary.  Both collectives are inside the timed region.
+
+value = all ranks' firm-month rows / max-over-ranks time (weak scaling).  At N=1 the line
+also carries the C5 per-rank shard through ShardedStep (`c5_rank_shard`, the N=1 point of
+the C5 scaling curve); at N>1 it also carries the headline panel weak-scaled
+(`headline_weak`, 600 months x 5,000 firms per rank, same exchanges).
 """
 import argparse
 import json
@@ -27,6 +37,8 @@ import torch  # noqa: E402
 
 METRIC = "firm-month rows/sec (and % HBM roofline) for full FM pass at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+C5_MONTHS, C5_FIRMS, C5_SEED = 12500, 20000, 20150101   # per rank (C5 = 100,000 months at N=8)
+B_ROW = 15 * 8 + 8 + 1   # input bytes of a firm-month row: 15 FP64 columns, me, the NYSE flag
 
 
 def parse():
@@ -34,16 +46,87 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--months", type=int, default=600, help="months per GPU")
-    ap.add_argument("--firms", type=int, default=5000)
+    ap.add_argument("--workload", choices=("headline", "c5"), default=None,
+                    help="default: headline at N=1, c5 at N>1")
+    ap.add_argument("--months", type=int, default=600, help="headline months per GPU")
+    ap.add_argument("--firms", type=int, default=5000, help="headline firms")
+    ap.add_argument("--c5-months", type=int, default=C5_MONTHS, help="c5 months per GPU")
+    ap.add_argument("--c5-firms", type=int, default=C5_FIRMS)
+    ap.add_argument("--c5-steps", type=int, default=5, help="timed steps of the N=1 C5 shard")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-months", type=int, default=240, help="oracle CPU-baseline sample")
+    ap.add_argument("--cpu-procs", type=int, default=8, help="month-parallel CPU baseline processes")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-chars", action="store_true", help="skip the firm-characteristic stage")
     ap.add_argument("--check", action="store_true", help="verify one step against the oracle")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
-    ap.add_argument("--no-c5", action="store_true", help="skip the C5 per-rank shard measurement")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 per-rank shard at N=1")
+    ap.add_argument("--no-headline", action="store_true", help="skip headline_weak at N>1")
     return ap.parse_args()
+
+
+def timed_steps(step, steps, warmup, graph, world, dev):
+    """W untimed warm-up steps (>= 1: the static exchange buffers), HIP-graph capture, then
+    exactly `steps` replays bracketed by barrier + synchronize; max over ranks."""
+    for _ in range(max(1, warmup)):
+        step.eager()
+    torch.cuda.synchronize()
+    if graph:
+        step.capture()
+    for _ in range(2):
+        step.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        from fmcore import dist as D
+        dt = D.max_over_ranks(dt, dev)
+    return dt, out
+
+
+def make_step(T_loc, N, seed, world, rank, dev, E, LW):
+    from fmcore.step import ShardedStep
+    panel = E.panel_synthetic(T_loc, N, seed, month0=rank * T_loc, device=dev)
+    T_glob = T_loc * world
+    # chunk the Gram by the GLOBAL panel so per-month sums are identical for any rank count
+    panel.chunk_rows = E.default_chunk_rows(T_glob * N, T_glob, N)
+    step = ShardedStep(panel, LW.PipelineConfig(), LW.table2_models(), world=world, rank=rank,
+                       seg_lo=rank * T_loc, seg_hi=(rank + 1) * T_loc, global_months=T_glob,
+                       counts=[T_loc] * world)
+    return panel, step
+
+
+def kernel_roofline(step, panel, E, steps):
+    """Per-kernel device times and the roofline of the dominant kernel.  Eager steps outside
+    the timed region fill engine.LAST_LAUNCH; each panel-sized launch is then re-issued back
+    to back on its stream (E.time_launch, HIP events: no launch gaps)."""
+    timer = E.KernelTimer()
+    with timer:
+        for _ in range(steps):
+            step.eager()
+    torch.cuda.synchronize()
+    kern = {tag: timer.avg_ms(tag) for tag in timer.names()}
+    tags = ("fm_select_cuts", "fm_select_cuts[nyse]", "fm_gram", "fm_universe", "fm_solve", "fm_ts_fused",
+            "fm_ts_fused[pred]")
+    reps = 20 if panel.nrows <= 10_000_000 else 3
+    dev_ms = {t: E.time_launch(t, reps) for t in tags if t in E.LAST_LAUNCH}
+    rows, C = panel.nrows, panel.ncols
+    # algorithmic HBM bytes per launch (DESIGN.md §4): every panel column once (8 B per value)
+    # and, for the Gram, the universe level byte
+    cand = {"fm_select_cuts": rows * C * 8, "fm_gram": rows * (C * 8 + 1)}
+    dom = max((t for t in cand if t in dev_ms), key=lambda k: dev_ms[k])
+    dom_ms = dev_ms[dom]
+    achieved = cand[dom] / (dom_ms * 1e-3) / 1e9
+    return dom, dom_ms, cand[dom], achieved, dev_ms, kern
 
 
 def main():
@@ -56,75 +139,31 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
-    from fmcore import dist as D
     from fmcore import engine as E
     from fmcore import lewellen as LW
-    from fmcore.step import ShardedStep
 
-    cfg = LW.PipelineConfig()
-    model_cols = LW.table2_models()
-    T_loc, N = args.months, args.firms
+    workload = args.workload or ("headline" if world == 1 else "c5")
+    if workload == "headline":
+        T_loc, N, seed = args.months, args.firms, args.seed
+        wl = ("C3+C4 full pass per GPU: 600 months x 5000 firms x 15 chars; winsorize 1/99 -> "
+              "NYSE universes -> M1/M2/M3 x 3 universes + Fig-1 x 2 -> NW(4) -> rolling 120/60 -> "
+              "lagged-rolling forecasts + predictive-slope FM")
+    else:
+        T_loc, N, seed = args.c5_months, args.c5_firms, C5_SEED
+        wl = (f"C5 month-sharded: {T_loc} months x {N} firms x 15 chars per GPU of a {T_loc * world}-month "
+              f"panel (N=8: 100,000 x 20,000 x 15); local pass -> RCCL all-gather of records -> "
+              f"time series on the gathered series -> RCCL all-reduce of predictive records")
+    panel, step = make_step(T_loc, N, seed, world, rank, dev, E, LW)
     T_glob = T_loc * world
-    panel = E.panel_synthetic(T_loc, N, args.seed, month0=rank * T_loc, device=dev)
-    # chunk the Gram by the GLOBAL panel so per-month sums are identical for any rank count
-    panel.chunk_rows = E.default_chunk_rows(T_glob * N, T_glob, N)
     rows_local = T_loc * N
-    step = ShardedStep(panel, cfg, model_cols, world=world, rank=rank, seg_lo=rank * T_loc,
-                       seg_hi=(rank + 1) * T_loc, global_months=T_glob, counts=[T_loc] * world)
-    for _ in range(max(1, args.warmup)):   # >= 1: allocates the static exchange buffers
-        step.eager()
-    torch.cuda.synchronize()
-    if not args.no_graph:
-        # capture (on a side stream, as torch.cuda.graph requires); the eager warm-up has
-        # filled every host-side cache, so the captured launches are exactly a step's kernels
-        step.capture()
-    for _ in range(2):
-        step.replay()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step.replay()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        dt = D.max_over_ranks(dt, dev)
-    # per-kernel device times (HIP events on the launch stream), from eager steps outside
-    # the timed region: they feed the roofline of the dominant kernel
-    timer = E.KernelTimer()
-    with timer:
-        for _ in range(max(3, min(args.steps, 10))):
-            step.eager()
-    torch.cuda.synchronize()
+    dt, out = timed_steps(step, args.steps, args.warmup, not args.no_graph, world, dev)
     gres, summ, psumm = out
-    nfit = int(((gres.status & 1) != 0).sum().item())
-
-    # roofline of the dominant kernel: per-launch algorithmic bytes / its device time, the
-    # latter from the latest launch re-issued back to back (E.time_launch: no launch gaps)
-    C = panel.ncols
-    kern = {}
-    for tag in timer.names():
-        kern[tag] = timer.avg_ms(tag)   # events around each eager launch (incl. launch gaps)
-    tags = ("fm_select_cuts", "fm_gram", "fm_universe", "fm_solve", "fm_ts_fused", "fm_ts_fused[pred]")
-    dev_ms = {t: E.time_launch(t) for t in tags if t in E.LAST_LAUNCH}
-    # algorithmic HBM bytes per launch: every panel column once (8 B per
-    # value), the universe level byte, and the month tables written (cuts, pivots, Gram
-    # partials); fm_select alone reads the columns only
-    cand = {"fm_select_cuts": rows_local * C * 8, "fm_gram": rows_local * (C * 8 + 1)}
-    dom = max((t for t in cand if t in dev_ms), key=lambda k: dev_ms[k])
-    dom_ms = dev_ms[dom]
-    achieved = cand[dom] / (dom_ms * 1e-3) / 1e9
-    traffic = _pmc_traffic(dom)
-    # whole pass: every input byte of a firm-month row -- the C FP64 columns,
-    # me (FP64) and the NYSE flag -- over the measured step time
-    b_row = C * 8 + 8 + 1
+    nfit = int(((gres.status & 1) != 0).sum().item())   # fitted (month, problem) pairs, all ranks
+    ksteps = max(3, min(args.steps, 10)) if workload == "headline" else 2
+    dom, dom_ms, dom_bytes, achieved, dev_ms, kern = kernel_roofline(step, panel, E, ksteps)
+    traffic = _pmc_traffic(dom) if workload == "headline" else None
     ms_step = dt / args.steps * 1e3
-    whole = rows_local * b_row / (ms_step * 1e-3) / 1e9
+    whole = rows_local * B_ROW / (ms_step * 1e-3) / 1e9   # per rank (each rank reads its shard)
 
     stream = _stream_copy_gbs(dev)
     result = {
@@ -134,94 +173,122 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (counter-hash panel generated in HBM, Table-1 moments, t2 tails, 2% NaN)",
         "config": {
-            "workload": "C3+C4 full pass per GPU: 600 months x 5000 firms x 15 chars; winsorize 1/99 -> "
-                        "NYSE universes -> M1/M2/M3 x 3 universes + Fig-1 x 2 -> NW(4) -> rolling 120/60 -> "
-                        "lagged-rolling forecasts + predictive-slope FM",
-            "months_per_gpu": T_loc, "firms": N, "chars": C, "problems_per_month": gres.nprob,
-            "global_months": T_glob, "parallelism": f"month-sharded x{world}, RCCL all-gather of records",
+            "workload": wl, "months_per_gpu": T_loc, "firms": N, "chars": panel.ncols,
+            "problems_per_month": gres.nprob, "global_months": T_glob, "seed": seed,
+            "parallelism": f"month-sharded x{world}" + (", RCCL all-gather of records + all-reduce of "
+                                                        "predictive records (timed)" if world > 1 else ""),
         },
         "regressions_per_s": nfit * args.steps / dt,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic["bytes"] if traffic else None,
-                     "traffic_ratio": traffic["bytes"] / cand[dom] if traffic else None,
+                     "traffic_ratio": traffic["bytes"] / dom_bytes if traffic else None,
                      "traffic_source": traffic["source"] if traffic else None,
-                     "bytes_per_launch": cand[dom], "avg_launch_ms": dom_ms,
+                     "bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms,
                      "measured_copy_peak": stream, "frac_of_measured_copy": achieved / stream,
-                     "whole_pass": {"bytes_per_row": b_row, "achieved": whole, "frac": whole / HBM_PEAK_GBS,
-                                    "ms_per_step": ms_step}},
+                     "whole_pass": {"bytes_per_row": B_ROW, "achieved": whole, "frac": whole / HBM_PEAK_GBS,
+                                    "ms_per_step": ms_step, "per": "rank"}},
         "kernel_ms": {k: round(v, 4) for k, v in dev_ms.items()},
         "lib_sha16": _lib_sha(),
         "kernel_ms_eager_events": {k: round(v, 4) for k, v in kern.items()},
         "graph": not args.no_graph,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if world > 1:
+        result["scaling_note"] = ("value at N>1 is the C5 workload; its N=1 point is the N=1 line's "
+                                  "c5_rank_shard.rows_per_s (same per-rank shard), the headline's "
+                                  "weak-scaled rate is headline_weak.value")
+    if args.check and rank == 0 and world == 1 and workload == "headline":
+        result["check"] = check_against_oracle(panel, gres, summ, args, LW)
+    if rank == 0 and world == 1 and workload == "headline" and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(panel, args, LW)
+    del step, panel, out, gres, summ, psumm
+    E.LAST_LAUNCH.clear()
+    torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_chars:
         result["firm_chars"] = firm_chars_stage(args, E)
-    if args.check and rank == 0 and world == 1:
-        result["check"] = check_against_oracle(panel, gres, summ, args, LW)
-    if rank == 0 and world == 1 and not args.no_c5:
-        del panel
+        E.LAST_LAUNCH.clear()
         torch.cuda.empty_cache()
-        result["c5_rank_shard"] = c5_shard_stage(args, E, LW)
+    if world == 1 and workload == "headline" and not args.no_c5:
+        result["c5_rank_shard"] = c5_shard_stage(args, E, LW, dev)
+    if world > 1 and workload == "c5" and not args.no_headline:
+        p2, s2 = make_step(args.months, args.firms, args.seed, world, rank, dev, E, LW)
+        d2, o2 = timed_steps(s2, args.steps, args.warmup, not args.no_graph, world, dev)
+        rows2 = args.months * args.firms
+        result["headline_weak"] = {"value": rows2 * world * args.steps / d2, "unit": "firm-month rows/s",
+                                   "ms_per_step": d2 / args.steps * 1e3, "months_per_gpu": args.months,
+                                   "firms": args.firms, "steps": args.steps,
+                                   "whole_pass_frac": rows2 * B_ROW / (d2 / args.steps) / 1e9 / HBM_PEAK_GBS}
+        del s2, p2, o2
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
-def c5_shard_stage(args, E, LW, reps=3):
+def c5_shard_stage(args, E, LW, dev):
     """C5 (BASELINE configs[4]: 100,000 months x 20,000 firms x 15 chars over 8 GPUs) at one
-    rank's size, as rank 4 of 8 runs it: its 12,500 months x 20,000 firms = 250M rows (30 GB
-    of FP64 columns) generated in HBM, the local pass (winsorize, universes, 11 problems per
-    month), then the time-series stage on the GATHERED 100,000-month series (FM means, NW,
-    rolling means, the predictive slopes of its own months + their summary).  The gathered
-    records are this pass's records tiled 8 times; the all-gather itself is replaced by one
-    device copy of the rank's rows.  Eager launches, HIP events around each stage."""
-    T, N, world, rank = 12500, 20000, 8, 4
-    p = E.panel_synthetic(T, N, 20150101, month0=rank * T)
+    rank's size through the same ShardedStep the N>1 c5 workload runs: 12,500 months x 20,000
+    firms = 250M rows (30 GB of FP64 columns) generated in HBM as rank 4 of 8 would, the local
+    pass and the time-series stage on its months, replayed from a HIP graph and timed like the
+    headline (the N=1 point of the c5 scaling curve).  Beside it, the time-series stage on the
+    100,000-month series the 8-rank all-gather assembles (this pass's records tiled 8 times),
+    which every rank of the 8-GPU run executes replicated."""
+    T, N, world8, rank8 = args.c5_months, args.c5_firms, 8, 4
+    from fmcore.step import ShardedStep
+    p = E.panel_synthetic(T, N, C5_SEED, month0=rank8 * T, device=dev)
+    step = ShardedStep(p, LW.PipelineConfig(), LW.table2_models(), seg_lo=rank8 * T, seg_hi=(rank8 + 1) * T)
+    dt, out = timed_steps(step, args.c5_steps, 1, not args.no_graph, 1, dev)
+    ms = dt / args.c5_steps * 1e3
+    rows = T * N
+    gres = out[0]
+    nfit = int(((gres.status & 1) != 0).sum().item())
+    # per-kernel device times of the C5 shard (eager step, launches re-issued back to back)
+    timer = E.KernelTimer()
+    with timer:
+        step.eager()
+    torch.cuda.synchronize()
+    kms = {t: round(E.time_launch(t, 3), 4) for t in ("fm_select_cuts", "fm_select_cuts[nyse]", "fm_gram",
+                                                        "fm_solve") if t in E.LAST_LAUNCH}
+    # the 100,000-month gathered series' time-series stage (replicated on every rank at N=8)
+    res = gres
+    lo, hi = rank8 * T, (rank8 + 1) * T
+    rec_g = res.rec.repeat(world8, 1, 1).contiguous()
+    st_g = res.status.repeat(world8, 1).contiguous()
+    g = E.FMResult(problems=res.problems, rec=rec_g, status=st_g, pmax=res.pmax, moments=res.moments,
+                   mom_stride=res.mom_stride)
     cfg = LW.PipelineConfig()
-    mc = LW.table2_models()
-    lo, hi = rank * T, (rank + 1) * T
-    res = LW.local_stage(p, cfg, mc)[0]   # warm-up (plans, workspaces)
-    rec_g = res.rec.repeat(world, 1, 1).contiguous()
-    st_g = res.status.repeat(world, 1).contiguous()
 
-    def ts(r):
-        rec_g[lo:hi].copy_(r.rec)   # stand-in for the all-gather of the ranks' records
-        st_g[lo:hi].copy_(r.status)
-        g = E.FMResult(problems=r.problems, rec=rec_g, status=st_g, pmax=r.pmax, moments=r.moments,
-                       mom_stride=r.mom_stride)
-        ix, summ, roll, pred, pst = LW.time_series_stage(g, cfg, moments=r.moments, seg_lo=lo, seg_hi=hi)
+    def ts():
+        ix, summ, roll, pred, pst = LW.time_series_stage(g, cfg, moments=res.moments, seg_lo=lo, seg_hi=hi)
         E.summarize_predictive(pred, pst, cfg.nw_lags)
 
-    ts(res)
+    ts()
     torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(reps)]
-    for e in ev:
-        e[0].record()
-        r = LW.local_stage(p, cfg, mc)[0]
-        e[1].record()
-        ts(r)
-        e[2].record()
-    ev[-1][2].synchronize()
-    loc = sum(e[0].elapsed_time(e[1]) for e in ev) / reps
-    tsm = sum(e[1].elapsed_time(e[2]) for e in ev) / reps
-    ms = loc + tsm
-    rows = T * N
-    return {"rows": rows, "months": T, "gathered_months": T * world, "firms": N, "ms_per_pass": ms,
-            "ms_local": loc, "ms_ts_100k": tsm, "rows_per_s": rows / (ms * 1e-3),
-            "whole_pass_frac": rows * (15 * 8 + 8 + 1) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "note": "eager launches; rank 4 of the 8-GPU C5 split (local pass + time series on the "
-                    "100,000-month gathered series; the all-gather is not timed)"}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        ts()
+    e1.record()
+    e1.synchronize()
+    tsm = e0.elapsed_time(e1) / 3
+    out_d = {"rows": rows, "months": T, "firms": N, "seed": C5_SEED, "steps": args.c5_steps,
+             "ms_per_pass": ms, "rows_per_s": rows / (ms * 1e-3), "regressions_per_s": nfit / (ms * 1e-3),
+             "whole_pass_frac": rows * B_ROW / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel_ms": kms,
+             "ms_ts_gathered_100k": tsm,
+             "note": "fmcore.step.ShardedStep at world 1 (HIP graph replay, timed like the headline): the "
+                     "N=1 point of the c5 workload; ms_ts_gathered_100k = the time-series stage on the "
+                     "100,000-month series an 8-rank all-gather assembles (run replicated per rank)"}
+    del step, p, out, gres, res, rec_g, st_g, g
+    E.LAST_LAUNCH.clear()
+    torch.cuda.empty_cache()
+    return out_d
 
 
 def _stream_copy_gbs(dev, nbytes=1 << 30, reps=10):
@@ -354,6 +421,24 @@ def cpu_baseline(panel, args, LW):
            "seconds": dt,
             "sample": f"first {S} months x {args.firms} firms of the same panel, full pass "
                       f"(11 problems/month, rolling, forecasts), oracle/fm_oracle.py, 1 BLAS thread"}
+    # optional month-parallel variant: all months of the panel, one contiguous
+    # month block per worker process, 1 BLAS thread each
+    if args.cpu_procs > 1:
+        from oracle import month_parallel as MP
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            avail = os.cpu_count() or 1
+        procs = max(1, min(args.cpu_procs, avail, 16))
+        n_all = panel.nrows
+        cols_all = {name: panel.cols[i].cpu().numpy() for i, name in enumerate(panel.names)}
+        sec, _ = MP.run(cols_all, panel.seg_off_h, panel.me.cpu().numpy(),
+                        panel.nyse.cpu().numpy().astype(bool), models, procs)
+        out["month_parallel"] = {"value": n_all / sec, "unit": "firm-month rows/s", "cores": procs,
+                                 "kind": "port", "seconds": sec,
+                                 "sample": f"all {panel.nseg} months x {args.firms} firms, {procs} processes x "
+                                           f"1 BLAS thread, one contiguous month block each "
+                                           f"(oracle/month_parallel.py)"}
     # the port vs the reference itself, timed side by side in the build container
     # (tools/ref_vs_port_timing.py -> profiles/ref_vs_port.json; the reference never travels)
     rp = os.path.join(ROOT, "profiles", "ref_vs_port.json")

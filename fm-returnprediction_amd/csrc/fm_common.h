@@ -116,6 +116,29 @@ __device__ __forceinline__ double hw_min(double a, double b) {
     return r;
 }
 
+// Error-free sum a + b = s + e (Knuth TwoSum; the library builds with -ffp-contract=off, so
+// no operation below is fused or reassociated).
+__device__ __forceinline__ double two_sum(double a, double b, double* e) {
+    const double s = a + b;
+    const double bp = s - a;
+    *e = (a - (s - bp)) + (b - bp);
+    return s;
+}
+
+// Compensated running sum (s + c): adding and later removing a term far larger than the
+// others leaves O(eps^2) of it behind instead of ulp(term) -- the sliding window sums of the
+// rolling means (pandas roll_mean keeps a Kahan compensation for the same reason).
+struct CSum {
+    double s = 0.0, c = 0.0;
+    __device__ __forceinline__ void add(double x) {
+        double e;
+        s = two_sum(s, x, &e);
+        c += e;
+    }
+    __device__ __forceinline__ double value() const { return s + c; }
+    __device__ __forceinline__ void reset() { s = c = 0.0; }
+};
+
 // number of set bits of `mask` strictly below this lane
 __device__ __forceinline__ int mask_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),

@@ -94,7 +94,8 @@ struct GramShape {
     static constexpr int ZW = 16 * NT;
     static constexpr int RS = ZW + 1;              // LDS row stride (doubles)
     static constexpr int TR = WAVE;                // rows per wave tile (one per lane)
-    static constexpr int WT = TR * RS;             // one wave's sorted tile
+    static constexpr int TPAD = 4;                 // pad rows after each wave's tile (see run)
+    static constexpr int WT = (TR + TPAD) * RS;    // one wave's sorted tile + its pad rows
     static constexpr int PK = ZW * (ZW + 1) / 2;   // packed upper triangle
     static constexpr int NI = NT == 1 ? 3 : BlockPairs<8>::NI;   // 4x4x4 MFMAs per 4-row group
 };
@@ -282,9 +283,9 @@ struct GramWave {
                     for (int g = 0; g < n; g += 4) {
                         const double Ar = An;
                         const int rn = g + 4 < n ? off + g + 4 : off + n;
-                        // rows past the tile end (< 3 of them: lanes of rows past a
-                        // bucket's count) read the next wave's tile or the zero rows that
-                        // follow the last one, and are masked below
+                        // rows past the tile end (rn + kr <= TR + 3: lanes of rows past a
+                        // bucket's count) read this wave's own TPAD pad rows, never another
+                        // wave's tile; their (unwritten) values are masked below
                         An = rd[rn * RS];
                         const double A = kr < n - g ? Ar : 0.0;
                         const double B1 = dpp_f64<0x12C>(A), B2 = dpp_f64<0x128>(A);

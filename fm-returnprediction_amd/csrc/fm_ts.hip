@@ -339,32 +339,32 @@ __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t 
     const int ib = c0 + g * RPT;
     if (k >= kmax || ib >= hi) return;
     const int j0 = ib - window + 1 < 0 ? 0 : ib - window + 1;
-    double sm = 0.0;
+    CSum sm;   // compensated: an outlier leaving the window leaves no ulp(outlier) behind
     int c = 0;
     for (int j = j0; j <= ib; ++j) {
         const double x = xs[(j - lo) * RKS + k];
         if (isfinite(x)) {   // pandas rolling: +-inf -> NaN (Window._prep_values)
-            sm += x;
+            sm.add(x);
             ++c;
         }
     }
-    out[((int64_t)p * nseg + ib) * kmax + k] = c >= minp ? sm / (double)c : NAN;
+    out[((int64_t)p * nseg + ib) * kmax + k] = c >= minp ? sm.value() / (double)c : NAN;
     for (int i = ib + 1; i < ib + RPT && i < hi; ++i) {
         const double xi = xs[(i - lo) * RKS + k];
         if (isfinite(xi)) {
-            sm += xi;
+            sm.add(xi);
             ++c;
         }
         const int jo = i - window;   // leaves the window
         if (jo >= 0) {
             const double xo = xs[(jo - lo) * RKS + k];
             if (isfinite(xo)) {
-                sm -= xo;
+                sm.add(-xo);
                 --c;
             }
         }
-        if (c == 0) sm = 0.0;
-        out[((int64_t)p * nseg + i) * kmax + k] = c >= minp ? sm / (double)c : NAN;
+        if (c == 0) sm.reset();
+        out[((int64_t)p * nseg + i) * kmax + k] = c >= minp ? sm.value() / (double)c : NAN;
     }
 }
 
@@ -825,43 +825,54 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
     __syncthreads();
     // per-column inclusive prefix sums of the finite values and their counts over the staged
     // rows (each output is then a difference of two prefixes: no serial window sums).  A
-    // column's rows are split over 16 threads: local scans, then the 16 block totals.
-    double* ps = rl + nq * PM;                        // [nsrc][PM] prefix sums
+    // column's rows are split over 16 threads: local scans, then the 16 block totals.  The
+    // prefixes are double-double (high part in ps, low part in place of the staged value):
+    // a prefix difference then loses nothing to an outlier that entered before both ends,
+    // where a plain prefix would leave ulp(outlier) in every later window.
+    double* ps = rl + nq * PM;                        // [nsrc][PM] prefix sums (high part)
+    double* pl = xs;                                  // [nsrc][PM] low part (overwrites xs)
     int* pc = reinterpret_cast<int*>(ps + nsrc * PM);  // [nsrc][PM] prefix counts
     for (int kb = 0; kb < PM; kb += 16) {
         const int k = kb + (tid >> 4), part = tid & 15;   // 16 columns x 16 parts at a time
         const int per = (nsrc + 15) / 16;
         const int a0 = part * per, a1 = a0 + per < nsrc ? a0 + per : nsrc;
-        double sm = 0.0;
+        CSum sm;
         int cn = 0;
         if (k < PM) {
             for (int j = a0; j < a1; ++j) {
                 const double x = xs[j * PM + k];
                 if (isfinite(x)) {   // pandas rolling: +-inf -> NaN (Window._prep_values)
-                    sm += x;
+                    sm.add(x);
                     ++cn;
                 }
-                ps[j * PM + k] = sm;
+                ps[j * PM + k] = sm.s;
+                pl[j * PM + k] = sm.c;
                 pc[j * PM + k] = cn;
             }
         }
         // exclusive prefix of the 16 part totals (lanes of one 16-lane row group)
-        double bs = sm;
+        CSum bs = sm;
         int bc = cn;
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
-            const double ys = __shfl_up(bs, o, 16);
+            const double yh = __shfl_up(bs.s, o, 16);
+            const double yl = __shfl_up(bs.c, o, 16);
             const int yc = __shfl_up(bc, o, 16);
             if (part >= o) {
-                bs += ys;
+                bs.add(yh);
+                bs.c += yl;
                 bc += yc;
             }
         }
-        bs -= sm;
+        bs.add(-sm.s);
+        bs.c -= sm.c;
         bc -= cn;
         if (k < PM)
             for (int j = a0; j < a1; ++j) {
-                ps[j * PM + k] += bs;
+                double e;
+                const double h = two_sum(ps[j * PM + k], bs.s, &e);
+                ps[j * PM + k] = h;
+                pl[j * PM + k] += bs.c + e;
                 pc[j * PM + k] += bc;
             }
     }
@@ -870,11 +881,14 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
         const int q = e / PM, k = e - q * PM, i = q0 + q;
         const int jlo = i - a.window;                 // prefix just before the window
         double sm = ps[(i - j0) * PM + k];
+        double sl = pl[(i - j0) * PM + k];
         int cn = pc[(i - j0) * PM + k];
         if (jlo >= j0) {
             sm -= ps[(jlo - j0) * PM + k];
+            sl -= pl[(jlo - j0) * PM + k];
             cn -= pc[(jlo - j0) * PM + k];
         }
+        sm += sl;
         const double m = cn >= a.min_periods && cn > 0 ? sm / (double)cn : NAN;
         rl[q * PM + k] = m;
         if (i >= r0) a.roll[((int64_t)p * T + i) * PM + k] = m;

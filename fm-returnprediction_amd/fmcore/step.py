@@ -9,8 +9,10 @@ A step is three device phases with the two exchanges of SURVEY.md §8(e) between
   exchange 2    SUM all-reduce of the predictive records (each row has one owner)
   phase_pred    FM summary of the predictive slopes
 
-At world size 1 there is no exchange and the whole step can be replayed from ONE HIP graph;
-otherwise each phase is its own graph (static buffers), with the exchanges between replays.
+Without exchanges (world size 1, no process group) the whole step can be replayed from ONE
+HIP graph; otherwise each phase is its own graph (static buffers), with the collectives
+between replays.  ``exchange=True`` at world size 1 (a 1-rank process group) runs the
+three-graph path with the collectives anyway -- the RCCL device path, executed on one GPU.
 """
 from __future__ import annotations
 
@@ -23,13 +25,22 @@ from . import lewellen as LW
 
 class ShardedStep:
     def __init__(self, panel: E.DevicePanel, cfg: LW.PipelineConfig, model_cols, world=1, rank=0,
-                 seg_lo=0, seg_hi=None, global_months=None, counts=None, group=None):
+                 seg_lo=0, seg_hi=None, global_months=None, counts=None, group=None, exchange=None):
         self.panel, self.cfg, self.model_cols = panel, cfg, model_cols
         self.world, self.rank, self.group = world, rank, group
         self.seg_lo = seg_lo
         self.seg_hi = seg_lo + panel.nseg if seg_hi is None else seg_hi
-        self.global_months = global_months or panel.nseg * world
+        if counts is not None and len(counts) != world:
+            raise ValueError("counts needs one month count per rank")
+        if global_months is None:
+            global_months = sum(counts) if counts is not None else panel.nseg * world
+        if counts is not None and global_months != sum(counts):
+            raise ValueError("global_months must equal sum(counts)")
+        self.global_months = global_months
         self.counts = counts
+        self.exchange = world > 1 if exchange is None else bool(exchange)
+        if world > 1 and not self.exchange:
+            raise ValueError("a sharded step (world > 1) needs its exchanges")
         self.rec_g = self.st_g = None
         self.graphs = None
         self._out = None
@@ -37,7 +48,7 @@ class ShardedStep:
     # ---- phases ------------------------------------------------------------------------
     def phase_local(self):
         res, names, cuts, level, bp = LW.local_stage(self.panel, self.cfg, self.model_cols)
-        if self.world > 1 and self.rec_g is None:
+        if self.exchange and self.rec_g is None:
             dev = res.rec.device
             self.rec_g = torch.empty((self.global_months,) + tuple(res.rec.shape[1:]), dtype=res.rec.dtype,
                                      device=dev)
@@ -46,12 +57,12 @@ class ShardedStep:
         return res
 
     def exchange_records(self, res):
-        if self.world > 1:
+        if self.exchange:
             D.gather_records_into(res.rec, res.status, self.rec_g, self.st_g, self.counts, self.group)
 
     def phase_ts(self, res):
         gres = res
-        if self.world > 1:
+        if self.exchange:
             gres = E.FMResult(problems=res.problems, rec=self.rec_g, status=self.st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
         ix, summ, roll, pred, pst = LW.time_series_stage(gres, self.cfg, moments=res.moments,
@@ -59,7 +70,7 @@ class ShardedStep:
         return gres, summ, pred, pst
 
     def exchange_pred(self, pred, pst):
-        if self.world > 1 and pred is not None:
+        if self.exchange and pred is not None:
             D.combine_predictive(pred, pst, self.group)
 
     def phase_pred(self, pred, pst):
@@ -78,9 +89,13 @@ class ShardedStep:
         return gres, summ, self.phase_pred(pred, pst)
 
     def capture(self):
-        """Capture the phases as HIP graphs (after an eager warm-up has filled every
-        host-side cache and allocated the static exchange buffers)."""
-        if self.world == 1:
+        """Capture the phases as HIP graphs.  Every host-side cache (chunk plans, model
+        plans) and the static exchange buffers must exist before capture: without a prior
+        eager() step, one is run here first."""
+        if self.exchange and self.rec_g is None:
+            self.eager()
+            torch.cuda.synchronize()
+        if not self.exchange:
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
                 res = self.phase_local()
@@ -90,15 +105,19 @@ class ShardedStep:
             self._out = (gres, summ, psumm)
             self._static = None
             return
-        ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        assert self.rec_g is not None and self.st_g is not None
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(ga):
             res = self.phase_local()
         self.exchange_records(res)
         with torch.cuda.graph(gb):
             gres, summ, pred, pst = self.phase_ts(res)
         self.exchange_pred(pred, pst)
-        with torch.cuda.graph(gc):
-            psumm = self.phase_pred(pred, pst)
+        gc, psumm = None, None
+        if pred is not None:   # no forecasts: no predictive phase to capture
+            gc = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gc):
+                psumm = self.phase_pred(pred, pst)
         self.graphs = (ga, gb, gc)
         self._static = (res, pred, pst)
         self._out = (gres, summ, psumm)
@@ -106,7 +125,7 @@ class ShardedStep:
     def replay(self):
         if self.graphs is None:
             return self.eager()
-        if self.world == 1:
+        if not self.exchange:
             self.graphs[0].replay()
             return self._out
         res, pred, pst = self._static
@@ -115,5 +134,6 @@ class ShardedStep:
         self.exchange_records(res)
         gb.replay()
         self.exchange_pred(pred, pst)
-        gc.replay()
+        if gc is not None:
+            gc.replay()
         return self._out

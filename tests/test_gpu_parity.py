@@ -596,6 +596,43 @@ def test_mid_panel_golden(R):
 
 
 # ---------------------------------------------------------------- full pipeline vs oracle
+def _compare_with_oracle(res, model_names, model_cols, ref, summary, rolling, pred_t, pst_t, pred_summary):
+    """Every problem of a device pass against oracle.pipeline_arrays on the same month-sorted
+    arrays: fitted-month lists and N exact; params, R2, rolling means, predictive slopes/R2
+    and every FM / predictive summary within the series-RMS tolerance."""
+    rec = res.rec.cpu().numpy()
+    st = res.status.cpu().numpy()
+    mean = summary.mean.cpu().numpy()
+    tstat = summary.tstat.cpu().numpy()
+    roll = rolling.cpu().numpy()
+    pred = pred_t.cpu().numpy()
+    pst = pst_t.cpu().numpy()
+    pmean = pred_summary.mean.cpu().numpy()
+    ptst = pred_summary.tstat.cpu().numpy()
+    assert len(res.problems) == len(ref)
+    for k, p in enumerate(res.problems):
+        name = model_names[p.model]
+        r = ref[(name, p.level)]
+        fitted = np.nonzero(st[:, k] & 1)[0]
+        assert np.array_equal(fitted, r["month"]), (name, p.level)
+        assert np.array_equal(rec[fitted, k, res.pmax + 1].astype(np.int64), r["N"])
+        assert_series_close(rec[fitted, k, res.pmax], r["R2"], f"{name} R2")
+        for j in range(p.K + 1):
+            assert_series_close(rec[fitted, k, j], r["params"][:, j], f"{name}/{p.level} param {j}")
+            assert_series_close(roll[k, :len(fitted), j], r["rolling"][:, j], f"{name} roll {j}")
+        # rows past the fitted-month count are written (NaN / status 0), never left stale
+        assert np.isnan(roll[k, len(fitted):]).all() and (pst[k, len(fitted):] == 0).all(), name
+        for j, x in enumerate(model_cols[name]):
+            assert scalar_close(mean[k, 1 + j], r["summary"][x][0], RTOL, 1e-12), (name, x)
+            assert scalar_close(tstat[k, 1 + j], r["summary"][x][1], RTOL, 1e-12), (name, x)
+        pf = np.nonzero(pst[k] & 1)[0]
+        assert np.array_equal(fitted[pf], r["pred_month"]), name
+        assert_series_close(pred[k, pf, 0], r["pred_slope"], f"{name} pred slope")
+        assert_series_close(pred[k, pf, 1], r["pred_R2"], f"{name} pred R2")
+        assert scalar_close(pmean[k, 0], r["pred_summary"][0], RTOL, 1e-12)
+        assert scalar_close(ptst[k, 0], r["pred_summary"][1], RTOL, 1e-12)
+
+
 def _pipeline_vs_oracle(E, T, N, seed, model_cols=None, fig1=True, standardize=False, tweak=None):
     from fmcore import lewellen as LW, synth
     model_cols = model_cols or LW.table2_models()
@@ -613,38 +650,8 @@ def _pipeline_vs_oracle(E, T, N, seed, model_cols=None, fig1=True, standardize=F
         models["Figure 1"] = ("retx", LW.FIG1_VARS, (0, 2))
     ref = O.pipeline_arrays(srt, seg_off, a["me"][panel.order], a["nyse"][panel.order].astype(bool), models,
                             None, standardize=standardize)
-    res = out.res
-    rec = res.rec.cpu().numpy()
-    st = res.status.cpu().numpy()
-    mean = out.summary.mean.cpu().numpy()
-    tstat = out.summary.tstat.cpu().numpy()
-    roll = out.rolling.cpu().numpy()
-    pred = out.pred.cpu().numpy()
-    pst = out.pred_status.cpu().numpy()
-    pmean = out.pred_summary.mean.cpu().numpy()
-    ptst = out.pred_summary.tstat.cpu().numpy()
-    assert len(res.problems) == sum(len(m[2]) for m in models.values())
-    for k, p in enumerate(res.problems):
-        name = out.model_names[p.model]
-        r = ref[(name, p.level)]
-        fitted = np.nonzero(st[:, k] & 1)[0]
-        assert np.array_equal(fitted, r["month"]), (name, p.level)
-        assert np.array_equal(rec[fitted, k, res.pmax + 1].astype(np.int64), r["N"])
-        assert_series_close(rec[fitted, k, res.pmax], r["R2"], f"{name} R2")
-        for j in range(p.K + 1):
-            assert_series_close(rec[fitted, k, j], r["params"][:, j], f"{name}/{p.level} param {j}")
-            assert_series_close(roll[k, :len(fitted), j], r["rolling"][:, j], f"{name} roll {j}")
-        # rows past the fitted-month count are written (NaN / status 0), never left stale
-        assert np.isnan(roll[k, len(fitted):]).all() and (pst[k, len(fitted):] == 0).all(), name
-        for j, x in enumerate(out.model_cols[name]):
-            assert scalar_close(mean[k, 1 + j], r["summary"][x][0], RTOL, 1e-12), (name, x)
-            assert scalar_close(tstat[k, 1 + j], r["summary"][x][1], RTOL, 1e-12), (name, x)
-        pf = np.nonzero(pst[k] & 1)[0]
-        assert np.array_equal(fitted[pf], r["pred_month"]), name
-        assert_series_close(pred[k, pf, 0], r["pred_slope"], f"{name} pred slope")
-        assert_series_close(pred[k, pf, 1], r["pred_R2"], f"{name} pred R2")
-        assert scalar_close(pmean[k, 0], r["pred_summary"][0], RTOL, 1e-12)
-        assert scalar_close(ptst[k, 0], r["pred_summary"][1], RTOL, 1e-12)
+    _compare_with_oracle(out.res, out.model_names, out.model_cols, ref, out.summary, out.rolling, out.pred,
+                         out.pred_status, out.pred_summary)
     return out
 
 
@@ -928,23 +935,33 @@ def _check_series_vs_restatement(res, summ, roll, cols=2, pred=None, pst=None, p
 
 def test_pipeline_headline_panel_full_size(E):
     """The bench's own panel (600 months x 5,000 firms x 15 characteristics, seed 1, generated
-    in HBM by fm_gen_panel) through the bench's step (ShardedStep, world size 1): six sampled
-    months' records for all 11 problems against the oracle on those months; FM summaries,
-    rolling means and the predictive-slope summary against the oracle's restatement applied
-    to the device's records."""
+    in HBM by fm_gen_panel) through the bench's step (ShardedStep, world size 1, eager and
+    HIP-graph replay) against oracle.pipeline_arrays on the SAME panel: all 600 months x 11
+    problems -- fitted months and N exact; params, R2, rolling means, predictive slopes and
+    every FM / predictive summary from the oracle's own records within the tolerance."""
     import torch
     from fmcore import lewellen as LW
     from fmcore.step import ShardedStep
     T, N, seed = 600, 5000, 1
     panel = E.panel_synthetic(T, N, seed)
-    step = ShardedStep(panel, LW.PipelineConfig(), LW.table2_models())
+    cfg = LW.PipelineConfig()
+    step = ShardedStep(panel, cfg, LW.table2_models())
     gres, summ, psumm = step.eager()
+    step.capture()
+    ggres, gsumm, gpsumm = step.replay()
     torch.cuda.synchronize()
+    assert _same(ggres.rec.cpu().numpy(), gres.rec.cpu().numpy())
+    assert _same(gpsumm.tstat.cpu().numpy(), psumm.tstat.cpu().numpy())
     names = list(LW.table2_models()) + ["Figure 1"]
-    _check_records_vs_oracle(gres, names, (0, 1, 150, 299, 451, T - 1), N, seed)
-    ix, summ2, roll, pred, pst = LW.time_series_stage(gres, LW.PipelineConfig())
+    model_cols = dict(LW.table2_models(), **{"Figure 1": LW.FIG1_VARS})
+    ix, summ2, roll, pred, pst = LW.time_series_stage(gres, cfg)
     assert _same(summ2.mean.cpu().numpy(), summ.mean.cpu().numpy())
-    _check_series_vs_restatement(gres, summ, roll, cols=3, pred=pred, pst=pst, psumm=psumm)
+    cols = {name: panel.cols[i].cpu().numpy() for i, name in enumerate(panel.names)}
+    models = {name: ("retx", xs, (0, 1, 2)) for name, xs in LW.table2_models().items()}
+    models["Figure 1"] = ("retx", LW.FIG1_VARS, (0, 2))
+    ref = O.pipeline_arrays(cols, panel.seg_off_h, panel.me.cpu().numpy(),
+                            panel.nyse.cpu().numpy().astype(bool), models, None)
+    _compare_with_oracle(gres, names, model_cols, ref, summ, roll, pred, pst, psumm)
 
 
 def test_time_series_stage_gathered_c5_length(E):
@@ -1257,3 +1274,49 @@ def test_expand_compustat_units_and_missing_ids():
     bad.loc[3, "report_date"] = pd.NaT
     with pytest.raises(ValueError):
         TC.expand_compustat_annual_to_monthly(bad)
+
+
+@pytest.mark.parametrize("fused", [True, False], ids=["ts_fused", "ts_per_stage"])
+def test_rolling_mean_outlier_months(E, fused):
+    """the rolling means slide (per-stage kernel) or difference prefix sums
+    (fused kernel).  A coefficient series with huge outliers (a near-singular month's slope)
+    must leave nothing behind once they leave the 120-row window: every window against its
+    exactly rounded mean (math.fsum), tolerance 1e-9 of the ordinary windows' scale."""
+    import math
+
+    import torch
+    T, K1, W, MP = 600, 3, 120, 60
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((T, K1))
+    x[200, 1] = 1e12
+    x[333, 2] = -3e11
+    x[334, 2] = 7e10
+    x[400, 0] = np.inf        # pandas rolling skips +-inf (Window._prep_values)
+    rs = K1 + 2
+    rec = np.zeros((T, 1, rs))
+    rec[:, 0, :K1] = x
+    dev = torch.device("cuda", 0)
+    rec_t = torch.from_numpy(rec).to(dev)
+    st_t = torch.ones((T, 1), dtype=torch.int32, device=dev)
+    res = E.FMResult(problems=[E.Problem(0, 0, K1 - 1)], rec=rec_t, status=st_t, pmax=K1)
+    if fused:
+        assert E.ts_fused_fits(T, K1, W)
+        _, _, roll, _, _ = E.ts_fused(rec_t, rs, rs, st_t, 1, 1, T, 1, rs, 4, window=W, min_periods=MP, pmax=K1)
+    else:
+        roll = E.rolling_result(res, E.compact_result(res), W, MP)
+    got = roll.cpu().numpy()[0]
+    for k in range(K1):
+        exp = np.full(T, np.nan)
+        big = np.zeros(T, dtype=bool)
+        for i in range(T):
+            w = x[max(0, i - W + 1):i + 1, k]
+            w = w[np.isfinite(w)]
+            if w.size >= MP:
+                exp[i] = math.fsum(w) / w.size
+                big[i] = np.abs(w).max() > 1e6
+        assert np.array_equal(np.isnan(got[:, k]), np.isnan(exp)), k
+        ok = ~np.isnan(exp)
+        scale = np.sqrt(np.mean(exp[ok & ~big] ** 2))
+        tol = RTOL * np.maximum(np.abs(exp), scale)
+        bad = np.flatnonzero(ok & ~(np.abs(got[:, k] - exp) <= tol))
+        assert bad.size == 0, (k, bad[:5], got[bad[:5], k], exp[bad[:5]])
