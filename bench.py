@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 per-rank shard at N=1")
     ap.add_argument("--no-headline", action="store_true", help="skip headline_weak at N>1")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="N>1 process group backend (nccl = RCCL; gloo only to rehearse on one GPU)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (with --dist-backend gloo)")
     return ap.parse_args()
 
 
@@ -123,6 +127,9 @@ def kernel_roofline(step, panel, E, steps):
     # algorithmic HBM bytes per launch: every panel column once (8 B per value)
     # and, for the Gram, the universe level byte
     cand = {"fm_select_cuts": rows * C * 8, "fm_gram": rows * (C * 8 + 1)}
+    if E.LAST_LAUNCH.get("fm_select_cuts", ("",))[0] == "fm_select_universe":
+        # long months: the universe rides the launch (+ me, the NYSE byte, the level byte)
+        cand["fm_select_cuts"] += rows * (8 + 1 + 1)
     dom = max((t for t in cand if t in dev_ms), key=lambda k: dev_ms[k])
     dom_ms = dev_ms[dom]
     achieved = cand[dom] / (dom_ms * 1e-3) / 1e9
@@ -134,11 +141,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     from fmcore import engine as E
     from fmcore import lewellen as LW
 

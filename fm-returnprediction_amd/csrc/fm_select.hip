@@ -215,6 +215,92 @@ __global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
 #ifndef FM_AB_LONG_MASKALL
 #define FM_AB_LONG_MASKALL 0   // timing builds only: mask every value slot
 #endif
+// One month of get_subsets (reference src/calc_Lewellen_2014.py:69-105) by an NW-wave
+// workgroup of the long-month kernel (one more grid column of fm_select_universe): the
+// pandas-lerp q_a / q_b quantiles of the month's NYSE rows' `me` (NaN skipped) by the
+// adaptive histogram select, then every row's level
+// (me >= cut_a) + (me >= cut_b) -- universe_kernel's computation (same exact order
+// statistics, same lerp), so the breakpoints and level bytes are identical.  The month's
+// `me` / NYSE bytes are STREAMED (L2-resident after the first pass: 45 KB) in UB-row batches
+// per pass instead of held in registers: the histogram select's own state already takes the
+// host kernel's register budget, and it must stay at four waves per SIMD.
+constexpr int UB = 8;
+template <int NW, int HBN, int CAP, typename Sm>
+__device__ __forceinline__ void universe_month_wg(const SelArgs& a, int s, Sm& sm) {
+    constexpr int NT = NW * WAVE;
+    const int tid = (int)threadIdx.x;
+    const int64_t r0 = a.seg_off[s];
+    const int L = (int)(a.seg_off[s + 1] - r0);
+    const int last = L > 0 ? L - 1 : 0;
+    const double* me = a.ume + r0;
+    const uint8_t* ny = a.unyse + r0;
+    const int nb = (L + NT * UB - 1) / (NT * UB);   // batches of UB rows per thread
+    // f(x) for this thread's rows v * NT + tid: x = me of a NYSE row, NaN otherwise
+    auto for_each = [&](auto&& f) {
+#pragma unroll 1
+        for (int b = 0; b < nb; ++b) {
+            double xb[UB];
+            uint8_t mb[UB];
+#pragma unroll
+            for (int q = 0; q < UB; ++q) {   // unconditional (clamped) loads, masked after
+                const int idx = (b * UB + q) * NT + tid;
+                const int ci = idx < L ? idx : last;
+                xb[q] = me[ci];
+                mb[q] = ny[ci];
+            }
+#pragma unroll
+            for (int q = 0; q < UB; ++q) {
+                const int idx = (b * UB + q) * NT + tid;
+                f(idx < L && mb[q] != 0 ? xb[q] : NAN);
+            }
+        }
+    };
+    int cnt = 0;
+    uint64_t kmn = SENT, kmx = 0;
+    for_each([&](double x) {
+        if (!isnan(x)) {
+            ++cnt;
+            const uint64_t k = dkey(x);
+            kmn = k < kmn ? k : kmn;
+            kmx = k > kmx ? k : kmx;
+        }
+    });
+    const int n = block_sum<NW>(cnt, sm.ints);
+    kmn = block_min_u64<NW>(kmn, sm.u64s);
+    kmx = block_max_u64<NW>(kmx, sm.u64s + NW);
+    double ca = NAN, cb = NAN;
+    if (n > 0) {   // block-uniform
+        int rk[4];
+        double g0, g1;
+        qranks(n, a.uq_a, 1, rk[0], rk[1], g0);
+        qranks(n, a.uq_b, 1, rk[2], rk[3], g1);
+        uint64_t ko[4] = {kmn, kmn, kmx, kmx};
+        hist_select_t<NW, HBN, CAP>(for_each, 4, rk, kmn, kmx, ko, sm);
+        ca = qlerp(kval(ko[0]), kval(ko[1]), g0, 1);
+        cb = qlerp(kval(ko[2]), kval(ko[3]), g1, 1);
+    }
+    if (threadIdx.x == 0) {
+        a.ucut_a[s] = ca;
+        a.ucut_b[s] = cb;
+    }
+    // level bytes of every row (NYSE or not; NaN me compares False)
+#pragma unroll 1
+    for (int b = 0; b < nb; ++b) {
+        double xb[UB];
+#pragma unroll
+        for (int q = 0; q < UB; ++q) {
+            const int idx = (b * UB + q) * NT + tid;
+            xb[q] = me[idx < L ? idx : last];
+        }
+#pragma unroll
+        for (int q = 0; q < UB; ++q) {
+            const int idx = (b * UB + q) * NT + tid;
+            if (idx < L) a.ulevel[r0 + idx] = (uint8_t)((xb[q] >= ca ? 1 : 0) + (xb[q] >= cb ? 1 : 0));
+        }
+    }
+    __syncthreads();   // the LDS is reused by the next unit
+}
+
 constexpr int LT = 512;
 constexpr int LNW = LT / WAVE;
 constexpr int LONG_VPT = 40;
@@ -237,6 +323,10 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
     const int tid = (int)threadIdx.x, lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
     const int s = blockIdx.x, c = blockIdx.y;
+    if (!MID && c == a.ncols) {   // fm_select_universe: the month's NYSE breakpoints + levels
+        universe_month_wg<LNW, HB, HCAP>(a, s, sm.hs);
+        return;
+    }
     const int64_t o = (int64_t)c * a.nseg + s;
     const int64_t r0 = a.seg_off[s];
     const int L = (int)(a.seg_off[s + 1] - r0);
@@ -468,8 +558,9 @@ template <int VPT>
 void launch_long(const SelArgs& a, hipStream_t st, bool mid) {
     if (mid)
         hipLaunchKernelGGL((select_long_kernel<VPT, true>), dim3(a.nseg, a.ncols), dim3(LT), 0, st, a);
-    else
-        hipLaunchKernelGGL((select_long_kernel<VPT, false>), dim3(a.nseg, a.ncols), dim3(LT), 0, st, a);
+    else   // with a universe (a.ume), one more grid column: its months' NYSE breakpoints
+        hipLaunchKernelGGL((select_long_kernel<VPT, false>), dim3(a.nseg, a.ncols + (a.ume ? 1 : 0)), dim3(LT), 0,
+                           st, a);
 }
 
 // the tail thresholds serve ranks < 512 from either end; row masks and middle ranks take the
@@ -1003,8 +1094,66 @@ extern "C" int fm_select_cuts(const double* cols, int64_t col_stride, int32_t nc
     return fm_select(&a, stream);
 }
 
+namespace fm {
+namespace {
+// fm_select, optionally with get_subsets' NYSE breakpoints + level bytes riding the two-wave
+// kernel's launch (u != NULL); whenever that kernel is not the path taken, the universe is
+// launched by fm_universe after the cuts instead (same outputs).
+int select_impl(const fm_select_args* args, const fm_universe_args* u, void* stream);
+}  // namespace
+}  // namespace fm
+
 extern "C" int fm_select(const fm_select_args* args, void* stream) {
+    return fm::select_impl(args, nullptr, stream);
+}
+
+extern "C" int fm_select_universe(const fm_select_args* args, const fm_universe_args* u, void* stream) {
     using namespace fm;
+    FM_REQUIRE(u != nullptr && u->me && u->nyse && u->cut_a && u->cut_b && u->level,
+               "fm_select_universe: null universe pointer");
+    FM_REQUIRE(u->q_a >= 0.0 && u->q_a <= 1.0 && u->q_b >= 0.0 && u->q_b <= 1.0,
+               "fm_select_universe: quantiles must be in [0,1]");
+    return select_impl(args, u, stream);
+}
+
+namespace fm {
+namespace {
+void set_universe(SelArgs& a, const fm_universe_args* u) {
+    a.ume = u->me;
+    a.unyse = u->nyse;
+    a.uq_a = u->q_a;
+    a.uq_b = u->q_b;
+    a.ucut_a = u->cut_a;
+    a.ucut_b = u->cut_b;
+    a.ulevel = u->level;
+}
+
+// the universe by its own launches (months past the fused paths): fm_universe's one-launch
+// kernel up to its register budget, else the row-masked pandas select of the NYSE `me` with
+// the level bytes (streaming path: any length)
+int universe_separately(const fm_select_args& x, const fm_universe_args* u, void* stream) {
+    if (x.max_seg_len <= 64 * ST)
+        return fm_universe(u->me, u->nyse, x.seg_off, x.nseg, x.max_seg_len, u->q_a, u->q_b, u->cut_a, u->cut_b,
+                           u->level, stream);
+    fm_select_args y{};
+    y.cols = u->me;
+    y.col_stride = 0;
+    y.ncols = 1;
+    y.seg_off = x.seg_off;
+    y.nseg = x.nseg;
+    y.max_seg_len = x.max_seg_len;
+    y.row_mask = u->nyse;
+    y.q_lo = u->q_a;
+    y.q_hi = u->q_b;
+    y.min_count = 1;
+    y.lerp_mode = 1;
+    y.lo = u->cut_a;
+    y.hi = u->cut_b;
+    y.level = u->level;
+    return select_impl(&y, nullptr, stream);
+}
+
+int select_impl(const fm_select_args* args, const fm_universe_args* u, void* stream) {
     FM_REQUIRE(args != nullptr, "fm_select: null args");
     const fm_select_args& x = *args;
     const double* cols = x.cols;
@@ -1024,11 +1173,23 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
               nullptr,     x.level};
     hipStream_t st = (hipStream_t)stream;
     const int vpt = (max_seg_len + ST - 1) / ST;
-    if (vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && x.mean == nullptr && nvalid != nullptr &&
-        !FM_AB_SELECT_STREAM) {
+    const bool long_path = vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && x.mean == nullptr &&
+                           nvalid != nullptr && !FM_AB_SELECT_STREAM;
+    // a universe rides the long-month kernel's launch (one more grid column) unless its tails
+    // need the histogram (MID) kernel; on every other path it is launched first, on its own
+    // (riding the two-wave kernel's persistent workgroups measured slower for short months:
+    // 118 vs 83 + 23 us on the bench panel, profiles/r04/v2_kbench_fused_universe.log)
+    const bool ride = u != nullptr && long_path && !long_is_mid(a, max_seg_len);
+    if (u != nullptr && !ride) {
+        const int rcu = universe_separately(x, u, stream);
+        if (rcu != FM_OK) return rcu;
+    }
+    if (long_path) {
         // past the 256-thread paths' register budget: the 512-thread register-resident
         // kernel (one read per unit); the streaming kernel redoes the units it marked
-        const int rc = launch_select_long(a, max_seg_len, st);
+        SelArgs al = a;
+        if (ride) set_universe(al, u);
+        const int rc = launch_select_long(al, max_seg_len, st);
         if (rc != FM_OK) return rc;
         FM_CHECK_LAUNCH("fm_select_cuts(long)");
         hipLaunchKernelGGL(select_stream_kernel<true>, dim3(256), dim3(ST), 0, st, a);
@@ -1088,6 +1249,9 @@ extern "C" int fm_select(const fm_select_args* args, void* stream) {
     FM_CHECK_LAUNCH("fm_select_cuts");
     return a.level ? fm_universe_level(cols, seg_off, nseg, (int64_t)max_seg_len * nseg, x.lo, x.hi, x.level, stream) : FM_OK;
 }
+
+}  // namespace
+}  // namespace fm
 
 extern "C" int fm_universe(const double* me, const uint8_t* nyse, const int64_t* seg_off, int32_t nseg,
                            int32_t max_seg_len, double q_a, double q_b, double* cut_a, double* cut_b,

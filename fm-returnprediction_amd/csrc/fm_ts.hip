@@ -818,9 +818,26 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
     double* xs = lds_d;                  // [nsrc][PM]
     double* rl = lds_d + nsrc * PM;      // [nq][PM]
     const double* rp = a.rec + (int64_t)p * a.r_prob;
-    for (int e = tid; e < nsrc * PM; e += FT) {
-        const int j = e / PM, k = e - j * PM;
-        xs[e] = rp[(int64_t)ixs[j0 + j] * a.r_seg + k];
+    {
+        // SB gathers per thread in flight together (clamped, unconditional loads; stores
+        // after): a load -> wait -> store loop pays one L2 round trip per element
+        constexpr int SB = 8;
+        const int ne = nsrc * PM;
+        for (int e0 = 0; e0 < ne; e0 += SB * FT) {
+            double v[SB];
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+                const int e = e0 + q * FT + tid;
+                const int ec = e < ne ? e : ne - 1;
+                const int j = ec / PM, k = ec - j * PM;
+                v[q] = rp[(int64_t)ixs[j0 + j] * a.r_seg + k];
+            }
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+                const int e = e0 + q * FT + tid;
+                if (e < ne) xs[e] = v[q];
+            }
+        }
     }
     __syncthreads();
     // per-column inclusive prefix sums of the finite values and their counts over the staged
@@ -904,7 +921,38 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
         const bool mine = row && s >= a.seg_lo && s < a.seg_hi;
         bool ok = false;
         double n = NAN, tb = 0.0, ty = 0.0, syy = NAN;
-        if (mine && i >= a.lag) {
+        if (K < 16) {   // block-uniform: lane b owns column b (b <= K) of the month's S
+            // the month's n, Syy and this lane's S column are loaded together, clamped to a
+            // valid row (a loop of dependent loads waits one round trip per regressor)
+            const bool have = mine && i >= a.lag;
+            const int sr = have ? s - a.seg_lo : 0;
+            const double* mo = a.moments + ((int64_t)sr * a.nprob + p) * a.mom_stride;
+            const double* S = mo + 1 + K1;
+            const int bc = b <= K ? b : 0;
+            double sc[15];
+#pragma unroll
+            for (int r = 0; r < 15; ++r) sc[r] = S[(r < K ? r : 0) * K1 + bc];
+            const double n0 = mo[0], syy0 = S[K * K1 + K];
+            if (have) {
+                const double* c = rl + (i - a.lag - q0) * PM;
+                bool bad = false;
+                for (int q = 0; q <= K; ++q) bad |= isnan(c[q]);
+                n = n0;
+                ok = !bad && n >= 2.0;
+                if (ok) {
+                    syy = syy0;
+                    const double cb = b < K ? c[1 + b] : 0.0;
+#pragma unroll
+                    for (int r = 0; r < 15; ++r) {
+                        if (r < K) {
+                            const double v = sc[r] * c[1 + r];
+                            if (b < K) tb += v * cb;
+                            else if (b == K) ty += v;
+                        }
+                    }
+                }
+            }
+        } else if (mine && i >= a.lag) {
             const double* c = rl + (i - a.lag - q0) * PM;
             bool bad = false;
             for (int q = 0; q <= K; ++q) bad |= isnan(c[q]);

@@ -54,6 +54,13 @@ class SelectArgs(C.Structure):
     ]
 
 
+class UniverseArgs(C.Structure):
+    _fields_ = [
+        ("me", _p), ("nyse", _p), ("q_a", _f64), ("q_b", _f64), ("cut_a", _p), ("cut_b", _p),
+        ("level", _p),
+    ]
+
+
 class TsArgs(C.Structure):
     _fields_ = [
         ("rec", _p), ("r_seg", _i64), ("r_prob", _i64), ("status", _p), ("s_seg", _i64),
@@ -93,6 +100,7 @@ _SIGS = {
     "fm_select_cuts": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _f64, _f64, _i32, _i32,
                               _p, _p, _p, _p, _p, _p]),
     "fm_select": (_i32, [C.POINTER(SelectArgs), _p]),
+    "fm_select_universe": (_i32, [C.POINTER(SelectArgs), C.POINTER(UniverseArgs), _p]),
     "fm_clip": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_standardize": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "fm_universe_level": (_i32, [_p, _p, _i32, _i64, _p, _p, _p, _p]),

@@ -216,10 +216,14 @@ class Cuts:
 
 
 def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols=None,
-                row_mask=None, moments=False, center=False, level=None, tag="fm_select_cuts"):
+                row_mask=None, moments=False, center=False, level=None, tag="fm_select_cuts",
+                universe=None):
     """Per (column, month) quantile cuts.  ``cols`` defaults to panel.cols.  ``moments``:
     also the clipped mean / sd; ``center``: also a Gram pivot inside the data; ``level``
-    (uint8 [rows], one column): every row's (x >= lo) + (x >= hi) (fm_select)."""
+    (uint8 [rows], one column): every row's (x >= lo) + (x >= hi) (fm_select).
+    ``universe`` = (q_a, q_b): also get_subsets' NYSE breakpoints and level bytes of the
+    panel's me / nyse rows in the same call (fm_select_universe: one launch on the two-wave
+    path); returns (Cuts, (cut_a, cut_b, level)) then."""
     src = panel.cols if cols is None else cols
     if src.dim() == 1:
         src = src.view(1, -1)
@@ -239,9 +243,21 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
                       q_hi=float(q_hi), min_count=int(min_count), lerp_mode=int(mode), lo=lo.data_ptr(),
                       hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=_ptr(mean), sd=_ptr(sd), center=_ptr(cen),
                       level=_ptr(level))
-    _kcall(tag, "fm_select", L.C.byref(sa), _stream())
-    _remember(tag, "fm_select", sa, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, level)
-    return Cuts(lo, hi, nv, mean, sd, cen)
+    if universe is None:
+        _kcall(tag, "fm_select", L.C.byref(sa), _stream())
+        _remember(tag, "fm_select", sa, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, level)
+        return Cuts(lo, hi, nv, mean, sd, cen)
+    ca = torch.empty(T, dtype=torch.float64, device=dev)
+    cb = torch.empty_like(ca)
+    ulev = torch.empty(panel.nrows, dtype=torch.uint8, device=dev)
+    ua = L.UniverseArgs(me=panel.me.data_ptr(), nyse=panel.nyse.data_ptr(), q_a=float(universe[0]),
+                        q_b=float(universe[1]), cut_a=ca.data_ptr(), cut_b=cb.data_ptr(), level=ulev.data_ptr())
+    _kcall(tag, "fm_select_universe", L.C.byref(sa), L.C.byref(ua), _stream())
+    # re-issued by time_launch with both structs (keep[1] holds the argument tuple)
+    LAST_LAUNCH[tag] = ("fm_select_universe", None,
+                        ((sa, ua, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, panel.me, panel.nyse,
+                          ca, cb, ulev), (L.C.byref(sa), L.C.byref(ua))))
+    return Cuts(lo, hi, nv, mean, sd, cen), (ca, cb, ulev)
 
 
 def clip(panel: DevicePanel, cuts: Cuts, out=None):
@@ -297,6 +313,9 @@ def universe(panel: DevicePanel, q_a=0.2, q_b=0.5):
 
 
 UNIVERSE_MAX_ROWS = 64 * 256   # fm_universe's register budget (one workgroup per month)
+# fm_select's long-month kernel: months of SELECT_LONG_MIN + 1 .. SELECT_LONG_MAX rows (no row
+# mask, no moments); fm_select_universe puts the universe months into its launch
+SELECT_LONG_MIN, SELECT_LONG_MAX = 24 * 256, 40 * 512
 
 
 def pilot_shift(panel: DevicePanel, cols=None):

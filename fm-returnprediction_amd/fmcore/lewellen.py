@@ -127,19 +127,30 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
     level, bp = None, None
     nlevels = 1
     models, names = build_models(panel, model_cols, y=y, fig1=cfg.fig1, universes=cfg.universes)
-    if cfg.universes:
-        # one launch, on the pass's own stream: a side-stream fork / join inside the captured
-        # graph cost more in cross-queue synchronization than the overlap saved
+    select = cfg.winsorize or cfg.standardize
+    # long months (C5's 20,000 firms: fm_select's long-month kernel) put the universe months
+    # into the winsorize launch (fm_select_universe: one more grid column); short ones keep
+    # fm_universe's own launch, on the pass's own stream (riding the two-wave kernel measured
+    # slower, and a side-stream fork / join inside the captured graph cost more in cross-queue
+    # synchronization than the overlap saved)
+    fused_universe = (cfg.universes and select and not cfg.standardize and
+                      E.SELECT_LONG_MIN < panel.max_seg_len <= E.SELECT_LONG_MAX)
+    if cfg.universes and not fused_universe:
         a, b, level = E.universe(panel)
         nlevels = 3
         bp = (a, b)
     add_back = None
-    if cfg.winsorize or cfg.standardize:
+    if select:
         mc = 5 if cfg.winsorize else 2 ** 31 - 1
         # standardize needs the exact clipped moments; otherwise the Gram pivot is the
         # select kernel's free center (midpoint of the cuts), and no moments pass runs
         cuts = E.select_cuts(panel, cfg.lower_percentile / 100, cfg.upper_percentile / 100, mc,
-                             E.LERP_NUMPY, moments=cfg.standardize, center=True)
+                             E.LERP_NUMPY, moments=cfg.standardize, center=True,
+                             universe=(0.2, 0.5) if fused_universe else None)
+        if fused_universe:
+            cuts, (a, b, level) = cuts
+            nlevels = 3
+            bp = (a, b)
         shift = cuts.center
         if cfg.standardize:
             shift, inv_scale, add_back = _standardize_params(panel, cuts, panel.col(y))

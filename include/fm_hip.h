@@ -191,6 +191,25 @@ typedef struct fm_select_args {
 
 int fm_select(const fm_select_args* args, void* stream);
 
+/* fm_select_universe: fm_select's cuts of `args` AND fm_universe's NYSE breakpoints + level
+ * bytes (get_subsets, reference src/calc_Lewellen_2014.py:69-105) over the same month
+ * segments (args->seg_off / nseg / max_seg_len), written to cut_a / cut_b [nseg] and level
+ * [rows]: the winsorize cuts of calc_Lewellen_2014.py:516-527 and the universes of :74-96 in
+ * one call.  Months of 6,145 .. 20,480 rows (fm_select's long-month path, no row mask, no
+ * moments) put the universe months into the same launch (one more grid column); otherwise
+ * the universe runs first, on its own (fm_universe, or the row-masked select + level bytes
+ * past 16,384 rows).  Outputs are identical to fm_select + fm_universe. */
+typedef struct fm_universe_args {
+    const double* me;            /* [rows] */
+    const uint8_t* nyse;         /* [rows] nonzero = NYSE row */
+    double q_a, q_b;             /* pandas groupby.quantile levels (0.2, 0.5) */
+    double* cut_a;               /* [nseg] */
+    double* cut_b;               /* [nseg] */
+    uint8_t* level;              /* [rows] (me >= cut_a) + (me >= cut_b) */
+} fm_universe_args;
+
+int fm_select_universe(const fm_select_args* args, const fm_universe_args* u, void* stream);
+
 int fm_clip(const double* src, double* dst, int64_t col_stride, int32_t ncols,
             const int64_t* seg_off, int32_t nseg, int64_t nrows,
             const double* lo, const double* hi, void* stream);

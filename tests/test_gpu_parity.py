@@ -314,6 +314,72 @@ def test_universe_kernel_vs_oracle(E):
         assert np.array_equal(level[off[t]:off[t + 1]], exp), t
 
 
+@pytest.mark.parametrize("maxlen", [6144, 9000, 20000, 24000])
+def test_select_universe_fused(E, maxlen):
+    """fm_select_universe: the winsorize cuts and get_subsets' NYSE breakpoints + level bytes
+    from one call.  Months <= 6,144 rows ride the two-wave kernel's launch (the universe
+    months streamed by its workgroups beside the winsorize units), months <= 20,480 rows the
+    long-month kernel's (one more grid column); longer ones take the streaming select and the
+    row-masked NYSE select.  Cuts must equal fm_select's alone bit for bit, breakpoints the
+    pandas lerp restatement and levels the reference's masks, over adversarial me months
+    (clusters, ties, NaN me, no NYSE row, every NYSE me NaN, 1-row months)."""
+    rng = np.random.default_rng(77)
+    segs, masks = [], []
+    for n in (1, 2, 7, 300, 2500, maxlen):
+        for kind in ("lognormal", "cluster", "ties"):
+            x = np.exp(rng.normal(5, 2, n)) if kind == "lognormal" else _hard_segment(rng, n, kind)
+            x[rng.random(n) < 0.05] = np.nan
+            segs.append(x)
+            masks.append(rng.random(n) < 0.4)
+    segs.append(np.exp(rng.normal(5, 2, 900)))
+    masks.append(np.zeros(900, dtype=bool))
+    x = np.exp(rng.normal(5, 2, 900))
+    m = rng.random(900) < 0.4
+    x[m] = np.nan
+    segs.append(x)
+    masks.append(m)
+    me = np.concatenate(segs)
+    ny = np.concatenate(masks).astype(np.uint8)
+    labels = np.repeat(np.arange(len(segs)), [len(x) for x in segs])
+    cols = [rng.standard_t(2, me.size) for _ in range(4)]
+    for c in cols:
+        c[rng.random(me.size) < 0.03] = np.nan
+    panel = E.panel_from_arrays(cols, ["a", "b", "c", "d"], labels, me=me, nyse=ny)
+    ref = E.select_cuts(panel, 0.01, 0.99, 5, E.LERP_NUMPY, center=True)
+    cuts, (a, b, level) = E.select_cuts(panel, 0.01, 0.99, 5, E.LERP_NUMPY, center=True, universe=(0.2, 0.5))
+    for x_, y_ in ((cuts.lo, ref.lo), (cuts.hi, ref.hi), (cuts.nvalid, ref.nvalid), (cuts.center, ref.center)):
+        assert _same(x_.cpu().numpy(), y_.cpu().numpy())
+    ua, ub, ul = E.universe(panel)
+    assert _same(a.cpu().numpy(), ua.cpu().numpy()) and _same(b.cpu().numpy(), ub.cpu().numpy())
+    assert np.array_equal(level.cpu().numpy(), ul.cpu().numpy())
+    a, b, level = a.cpu().numpy(), b.cpu().numpy(), level.cpu().numpy()
+    off = panel.seg_off_h
+    order = panel.order
+    for t in range(len(segs)):
+        xs = me[order][off[t]:off[t + 1]]
+        ms = ny[order][off[t]:off[t + 1]].astype(bool)
+        v = xs[ms & ~np.isnan(xs)]
+        ea = O.pandas_quantile(v, 0.2) if v.size else np.nan
+        eb = O.pandas_quantile(v, 0.5) if v.size else np.nan
+        assert _same([a[t]], [ea]) and _same([b[t]], [eb]), t
+        with np.errstate(invalid="ignore"):
+            exp = (xs >= ea).astype(np.uint8) + (xs >= eb).astype(np.uint8)
+        assert np.array_equal(level[off[t]:off[t + 1]], exp), t
+
+
+def test_select_universe_fused_bench_panel(E):
+    """The bench panel (600 x 5,000, generated in HBM): fused cuts / breakpoints / levels equal
+    the separate fm_select + fm_universe launches bit for bit."""
+    panel = E.panel_synthetic(600, 5000, 1)
+    ref = E.select_cuts(panel, 0.01, 0.99, 5, E.LERP_NUMPY, center=True)
+    ua, ub, ul = E.universe(panel)
+    cuts, (a, b, level) = E.select_cuts(panel, 0.01, 0.99, 5, E.LERP_NUMPY, center=True, universe=(0.2, 0.5))
+    for x_, y_ in ((cuts.lo, ref.lo), (cuts.hi, ref.hi), (cuts.nvalid, ref.nvalid), (cuts.center, ref.center),
+                   (a, ua), (b, ub)):
+        assert _same(x_.cpu().numpy(), y_.cpu().numpy())
+    assert np.array_equal(level.cpu().numpy(), ul.cpu().numpy())
+
+
 def test_pandas_quantile_bit_exact(E):
     g = load_npz("pct.npz")
     vals, off, ref = g["values"], g["offsets"], g["pd_quantile"]
