@@ -103,6 +103,7 @@ def make_step(T_loc, N, seed, world, rank, dev, E, LW):
     T_glob = T_loc * world
     # chunk the Gram by the GLOBAL panel so per-month sums are identical for any rank count
     panel.chunk_rows = E.default_chunk_rows(T_glob * N, T_glob, N)
+    panel.chunk_split = E.split_policy(T_glob)
     step = ShardedStep(panel, LW.PipelineConfig(), LW.table2_models(), world=world, rank=rank,
                        seg_lo=rank * T_loc, seg_hi=(rank + 1) * T_loc, global_months=T_glob,
                        counts=[T_loc] * world)

@@ -41,9 +41,10 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);   // wave-uniform (SGPR loops)
-    // chunks run last-month-first: fm_select streams the panel month by month, so the
-    // months it read last are still in the memory-side cache when they are read here
-    const int chunk = (int)gridDim.x - 1 - (int)blockIdx.x;
+    // default order last-month-first: fm_select streams the panel month by month, so the
+    // months it read last are still in the memory-side cache when they are read here; with
+    // a chunk_order (the split-month plan) the big chunks go first, the small ones fill in
+    const int chunk = a.chunk_order ? a.chunk_order[blockIdx.x] : (int)gridDim.x - 1 - (int)blockIdx.x;
     const int seg = a.chunk_seg[chunk];
     const int64_t r0 = a.chunk_row[2 * chunk], r1 = a.chunk_row[2 * chunk + 1];
     const int ncols = a.ncols, nseg = a.nseg;

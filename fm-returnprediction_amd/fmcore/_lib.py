@@ -41,7 +41,7 @@ class GramArgs(C.Structure):
         ("level", _p), ("nlevels", _i32),
         ("model_mask", _p), ("model_ymask", _p), ("nmodels", _i32),
         ("pattern_id", _p), ("npatterns", _i32),
-        ("partial", _p), ("flags", _p),
+        ("partial", _p), ("flags", _p), ("chunk_order", _p),
     ]
 
 

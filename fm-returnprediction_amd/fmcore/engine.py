@@ -123,6 +123,7 @@ class DevicePanel:
     nyse: Optional[torch.Tensor] = None  # [n] uint8
     order: Optional[np.ndarray] = None   # sorted row -> original positional row
     chunk_rows: Optional[int] = None     # Gram chunking override (sharded runs: global policy)
+    chunk_split: Optional[bool] = None   # split-month Gram plan (make_chunks_split) override
 
     @property
     def nrows(self):
@@ -416,6 +417,45 @@ def default_chunk_rows(total_rows, nseg, max_seg_len, target_chunks=512):
     return max(256, ((ch + 255) // 256) * 256)
 
 
+def split_policy(nseg):
+    """Whether the Gram takes the split-month plan (make_chunks_split) by default.  A grid of
+    whole months that is a few rounds of the chip's resident workgroup slots leaves the CUs
+    unevenly loaded (600 months cost as much as 768: profiles/r04/v1_size_scan.log), but the
+    3/4 + 1/4 split with the big chunks launched first measured -2 us on the Gram and +2 us on
+    the solve at the bench's 600 months (profiles/r04/v3_split_scan.log: -10 us at 512
+    months, +5 us at 768), so it is off; callers opt in with panel.chunk_split = True.
+    Callers that shard months pass the GLOBAL month count, like default_chunk_rows, so every
+    rank plans (and sums) identically."""
+    return False
+
+
+def make_chunks_split(seg_off_h, num=3, den=4, min_rows=256):
+    """Every month of >= min_rows rows as two chunks, rows [0, L*num/den) and the rest (a
+    function of the month's own length only, so sharding does not change its sums), else one.
+    Returns (seg, rows, off, order): the chunk arrays in month order (fm_solve sums a month's
+    chunks from seg_chunk_off) and the launch order for fm_gram's chunk_order -- every big
+    chunk first (last month first), then the small ones, which fill the slots the big ones
+    leave (longest-first scheduling evens the per-CU load)."""
+    T = len(seg_off_h) - 1
+    lens = np.diff(seg_off_h).astype(np.int64)
+    two = lens >= min_rows
+    nch = np.where(two, 2, 1).astype(np.int64)
+    off = np.zeros(T + 1, dtype=np.int32)
+    np.cumsum(nch, out=off[1:])
+    n = int(off[-1])
+    seg = np.repeat(np.arange(T, dtype=np.int32), nch)
+    rows = np.empty((n, 2), dtype=np.int64)
+    first = off[:-1].astype(np.int64)
+    cut = seg_off_h[:-1] + (lens * num) // den
+    rows[first, 0] = seg_off_h[:-1]
+    rows[first, 1] = np.where(two, cut, seg_off_h[1:])
+    sec = first[two] + 1
+    rows[sec, 0] = cut[two]
+    rows[sec, 1] = seg_off_h[1:][two]
+    order = np.concatenate([first[::-1], sec[::-1]]).astype(np.int32)
+    return seg, rows.reshape(-1), off, order
+
+
 def make_chunks(seg_off_h, chunk_rows):
     """Split every month into ceil(L / chunk_rows) near-equal chunks (depends only on the
     month's own length, so per-month arithmetic is independent of sharding)."""
@@ -440,17 +480,26 @@ class _Plan:
     chunk_row: torch.Tensor
     seg_chunk_off: torch.Tensor
     nchunks: int
+    order: Optional[torch.Tensor] = None   # fm_gram launch order (split plan) or None
 
 
 def _chunk_plan(panel: DevicePanel):
     cache = getattr(panel, "_chunk_cache", None)
     if cache is not None:
         return cache
-    ch = panel.chunk_rows or default_chunk_rows(panel.nrows, panel.nseg, panel.max_seg_len)
-    seg, rows, off = make_chunks(panel.seg_off_h, ch)
+    split = panel.chunk_split
+    if split is None:   # an explicit chunk_rows (a sharded caller's global policy) keeps it
+        split = panel.chunk_rows is None and split_policy(panel.nseg)
+    order = None
+    if split:
+        seg, rows, off, order = make_chunks_split(panel.seg_off_h)
+    else:
+        ch = panel.chunk_rows or default_chunk_rows(panel.nrows, panel.nseg, panel.max_seg_len)
+        seg, rows, off = make_chunks(panel.seg_off_h, ch)
     dev = panel.cols.device
     plan = _Plan(torch.from_numpy(seg).to(dev), torch.from_numpy(rows).to(dev),
-                 torch.from_numpy(off).to(dev), len(seg))
+                 torch.from_numpy(off).to(dev), len(seg),
+                 None if order is None else torch.from_numpy(order).to(dev))
     panel._chunk_cache = plan
     return plan
 
@@ -590,7 +639,8 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
             lo=_ptr(lo), hi=_ptr(hi), shift=_ptr(shift), inv_scale=_ptr(inv_scale),
             level=_ptr(level), nlevels=nlevels, model_mask=gpl.mm.data_ptr(),
             model_ymask=gpl.ym.data_ptr(), nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(),
-            npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr())
+            npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr(),
+            chunk_order=_ptr(plan.order))
         _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
         _remember("fm_gram", "fm_gram", ga, src, partial, flags, lo, hi, shift, inv_scale, level, plan, gpl)
         grec, gst, gmom = _solve_group(panel, src, gpl, partial, plan.seg_chunk_off, zw, nlevels, T, pmax,

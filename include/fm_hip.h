@@ -118,6 +118,10 @@ typedef struct fm_gram_args {
     double* partial;              /* [nchunks][nbuckets][zw*(zw+1)/2] packed upper triangle, zw = 16 or 32 */
     uint32_t* flags;              /* [nseg][nmodels] reserved (not written: fm_solve detects inf in
                                      X / y per problem from the Gram diagonal); zeroed by caller */
+    const int32_t* chunk_order;   /* [nchunks] chunk processed by workgroup b, or NULL: chunks in
+                                     reverse index order (the months fm_select streamed last, still
+                                     in the Infinity Cache, first).  Only the launch order: each
+                                     chunk's partial is the same either way */
 } fm_gram_args;
 
 typedef struct fm_solve_args {

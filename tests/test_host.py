@@ -216,3 +216,28 @@ def test_etl_month_codes_round_trip():
     back = pd.DatetimeIndex(X.code_to_month_end(c))
     assert list(back.strftime("%Y-%m-%d")) == ["1964-01-31", "1999-12-31", "2000-02-29", "2013-06-30",
                                                "1970-01-31"]
+
+
+def test_split_month_chunk_plan():
+    """make_chunks_split: every month of >= 256 rows as a 3/4 + 1/4 pair (own length only),
+    shorter ones whole; chunks tile each month exactly; the launch order is a permutation
+    with every big chunk first (last month first)."""
+    import numpy as np
+    from fmcore.engine import make_chunks_split, split_policy
+    lens = np.array([5000, 255, 256, 1, 7919, 0, 300])
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    seg, rows, coff, order = make_chunks_split(off)
+    rows = rows.reshape(-1, 2)
+    assert sorted(order.tolist()) == list(range(len(seg)))
+    for t in range(len(lens)):
+        cs = list(range(coff[t], coff[t + 1]))
+        assert all(seg[c] == t for c in cs)
+        assert len(cs) == (2 if lens[t] >= 256 else 1)
+        assert rows[cs[0], 0] == off[t] and rows[cs[-1], 1] == off[t + 1]
+        for a, b in zip(cs, cs[1:]):
+            assert rows[a, 1] == rows[b, 0]
+        if len(cs) == 2:
+            assert rows[cs[0], 1] - rows[cs[0], 0] == lens[t] * 3 // 4
+    nbig = len(lens)
+    assert list(order[:nbig]) == list(coff[:-1][::-1])
+    assert not split_policy(600) and not split_policy(12500)

@@ -18,6 +18,7 @@ for s in "$@"; do
     bench)   specs+=("bench:::500:::python bench.py --steps 20 $BENCH_ARGS");;
     quick)   specs+=("quick:::300:::python bench.py --no-cpu --no-chars --no-c5 --steps 20 $BENCH_ARGS");;
     scan)    specs+=("scan:::300:::python tools/size_scan.py");;
+    split)   specs+=("split:::300:::python tools/split_scan.py");;
     rehearse) specs+=("rehearse:::400:::python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --one-device --c5-months 400 --months 300");;
     kbench)  specs+=("kbench:::300:::python tools/kbench.py $KB_LIBS");;
     kstats)  specs+=("kstats:::500:::$PROF --kernel-trace --stats -d $R/gpurun_out/kt -o kt --output-format csv -- python3 $R/bench.py --no-cpu --no-chars --steps 10 $BENCH_ARGS");;
