@@ -460,6 +460,9 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
             for (int v = 0; v < VPT; ++v) {
                 wl += (int)__popcll(__ballot(xv[v] <= tlo));
                 wh += (int)__popcll(__ballot(xv[v] >= thi));
+                // counts in order: otherwise the compiler forms all 2 x VPT ballot masks first
+                // and spills them to VGPR lanes (~300 writelane / readlane VALU per wave)
+                asm volatile("" : "+s"(wl), "+s"(wh));
             }
             if (lane == 0) {
                 sm.wc[0][w] = wl;
@@ -736,10 +739,16 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
     const int64_t nunits = (int64_t)a.nseg * a.ncols;
     int64_t k = blockIdx.x;
     if (k >= nunits) return;   // block-uniform
+    // unit k = (month k / ncols, column k % ncols), walked by (month, column) steps of the
+    // grid size: no 64-bit division per unit (unit_of's emulated divisions cost ~45 scalar /
+    // vector instructions each, four per unit)
+    const int ncols = a.ncols;
+    const int G = (int)gridDim.x;
+    const int dS = G / ncols, dC = G - (G / ncols) * ncols;
+    int s_cur = (int)blockIdx.x / ncols;
+    int c_cur = (int)blockIdx.x - s_cur * ncols;
     double xv[VPH];
-    auto load = [&](int64_t kk) -> int {
-        const int64_t u = unit_of(a, kk);
-        const int s = (int)(u % a.nseg), c = (int)(u / a.nseg);
+    auto load = [&](int s, int c) -> int {
         const double* base = a.cols + (int64_t)c * a.col_stride;
         const int64_t r0 = a.seg_off[s];
         const int L = (int)(a.seg_off[s + 1] - r0);
@@ -757,8 +766,7 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
     };
     // finite min / max of this wave's half of unit u, re-read from memory: only the rare
     // pivot fallback (no finite cut midpoint) needs it, and by then xv holds the next unit
-    auto finite_range = [&](int64_t uu, double& m1, double& m2) {
-        const int s = (int)(uu % a.nseg), c = (int)(uu / a.nseg);
+    auto finite_range = [&](int s, int c, double& m1, double& m2) {
         const double* base = a.cols + (int64_t)c * a.col_stride + a.seg_off[s];
         const int Lu = (int)(a.seg_off[s + 1] - a.seg_off[s]);
         m1 = NAN;
@@ -774,11 +782,16 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
             m2 = hw_max(m2, xor_lanes_f64(m2, o));
         }
     };
-    int L = load(k);
+    int L = load(s_cur, c_cur);
     while (true) {
-        const int64_t u = unit_of(a, k);
+        const int64_t u = (int64_t)c_cur * a.nseg + s_cur;
         const int64_t kn = k + gridDim.x;
         const bool more = kn < nunits;
+        int s_nx = s_cur + dS, c_nx = c_cur + dC;
+        if (c_nx >= ncols) {
+            c_nx -= ncols;
+            ++s_nx;
+        }
         int Ln = 0;
         int row0 = h * WAVE + lane;
         asm volatile("" : "+v"(row0));
@@ -888,7 +901,7 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
                 sm.ni[h][2] = chi;
             }
             // xv is dead from here on: the next unit's loads fly during the candidate sorts
-            if (more) Ln = load(kn);
+            if (more) Ln = load(s_nx, c_nx);
             prefetched = true;
             __syncthreads();
             // ---- 4. one tail per wave over both halves' candidates
@@ -917,7 +930,7 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
             double cen = 0.5 * (lo + hi);
             if (!isfinite(cen)) {
                 double m1, m2;
-                finite_range(u, m1, m2);
+                finite_range(s_cur, c_cur, m1, m2);
                 if (lane == 0) sm.res[0] = m1, sm.res[1] = m2;
             }
             if (lane == 0) {
@@ -929,10 +942,10 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
         } else if (!isfinite(0.5 * (lo + hi))) {
             // wave 1's half of the finite range for the pivot fallback
             double m1, m2;
-            finite_range(u, m1, m2);
+            finite_range(s_cur, c_cur, m1, m2);
             if (lane == 0) sm.tv[0] = m1, sm.tv[1] = m2;
         }
-        if (more && !prefetched) Ln = load(kn);   // the next unit's loads fly across the barrier
+        if (more && !prefetched) Ln = load(s_nx, c_nx);   // the next unit's loads fly across the barrier
         __syncthreads();
         if ((ok || !apply) && a.center && !isfinite(0.5 * (lo + hi)) && threadIdx.x == 0) {
             // pivot fallback: the midpoint of the finite range (both halves), else 0
@@ -943,6 +956,8 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
         __syncthreads();   // LDS state is rewritten by the next unit
         if (!more) break;
         k = kn;
+        s_cur = s_nx;
+        c_cur = c_nx;
         L = Ln;
     }
 }
@@ -1041,9 +1056,15 @@ __global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const d
         xm[v] = idx < L ? x : NAN;
         if (idx < L && m != 0 && !isnan(x)) nb |= 1ull << v;
     }
+    // each pass re-forms the masked value (opaque to the optimizer): kept across the
+    // histogram passes, the per-value NaN tests become 2 x VPT SGPRs spilled to VGPR lanes
     auto for_each = [&](auto&& f) {
 #pragma unroll
-        for (int v = 0; v < VPT; ++v) f(((nb >> v) & 1ull) ? xm[v] : NAN);
+        for (int v = 0; v < VPT; ++v) {
+            double x = ((nb >> v) & 1ull) ? xm[v] : NAN;
+            asm volatile("" : "+v"(x));
+            f(x);
+        }
     };
     int cnt = 0;
     uint64_t kmn = SENT, kmx = 0;

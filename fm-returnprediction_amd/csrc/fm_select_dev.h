@@ -207,6 +207,17 @@ __device__ __forceinline__ uint32_t cnd_u32(uint64_t m, uint32_t if0, uint32_t i
     asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
     return r;
 }
+// The compile-time lane mask M in an SGPR pair, materialized right here (two s_mov_b32):
+// as plain constants the compiler hoists every stage's mask out of the unit loop and, short
+// of SGPRs, spills them to VGPR lanes -- a v_readlane pair (VALU) per bitonic stage instead
+// of two scalar moves.
+template <uint64_t M>
+__device__ __forceinline__ uint64_t lane_mask() {
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3" : "=s"(lo), "=s"(hi)
+                 : "i"((uint32_t)M), "i"((uint32_t)(M >> 32)));
+    return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ double cnd_f64(uint64_t m, double if0, double if1) {
     const uint64_t a = (uint64_t)__double_as_longlong(if0), b = (uint64_t)__double_as_longlong(if1);
     const uint32_t lo = cnd_u32(m, (uint32_t)a, (uint32_t)b);
@@ -270,7 +281,7 @@ __device__ __forceinline__ void bitonic_f64_stages(double (&v)[R]) {
             double p0, p1;
             xor_pair_f64<J>(v[r], p0, p1);
             const double mn = hw_min(p0, p1), mx = hw_max(p0, p1);
-            v[r] = cnd_f64(bitonic_min_mask<K, J, r>(), mx, mn);
+            v[r] = cnd_f64(lane_mask<bitonic_min_mask<K, J, r>()>(), mx, mn);
         });
     }
     if constexpr (J > 1) bitonic_f64_stages<R, K, J / 2>(v);
@@ -291,7 +302,7 @@ __device__ __forceinline__ void bitonic_u32_stages(uint32_t& v) {
     uint32_t p0, p1;
     xor_pair_u32<J>(v, p0, p1);
     const uint32_t mn = p0 < p1 ? p0 : p1, mx = p0 < p1 ? p1 : p0;
-    v = cnd_u32(bitonic_min_mask<K, J, 0>(), mx, mn);
+    v = cnd_u32(lane_mask<bitonic_min_mask<K, J, 0>()>(), mx, mn);
     if constexpr (J > 1) bitonic_u32_stages<K, J / 2>(v);
 }
 

@@ -915,37 +915,49 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
     // predictive slopes: a 16-lane group per row, lane b owns column b of each S row
     const int K = a.prob_k[p], K1 = K + 1;
     const int g = tid >> 4, b = tid & 15;
-    for (int i = r0 + g; i < r0 + RROWS; i += FT / 16) {     // uniform trip count (shuffles)
+    constexpr int NIT = RROWS / (FT / 16);   // rows per 16-lane group
+    // K < 16 (block-uniform): the month moments of ALL the group's rows are loaded up front
+    // (n, Syy and this lane's S column, clamped to a valid row), one round trip instead of one
+    // per row
+    double scq[NIT][15], n0q[NIT], syq[NIT];
+    if (K < 16) {
+        const int bc = b <= K ? b : 0;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int i = r0 + g + it * (FT / 16);
+            const int s = i < r1 ? ixs[i] : -1;
+            const bool have = i < r1 && s >= a.seg_lo && s < a.seg_hi && i >= a.lag;
+            const int sr = have ? s - a.seg_lo : 0;
+            const double* mo = a.moments + ((int64_t)sr * a.nprob + p) * a.mom_stride;
+            const double* S = mo + 1 + K1;
+#pragma unroll
+            for (int r = 0; r < 15; ++r) scq[it][r] = S[(r < K ? r : 0) * K1 + bc];
+            n0q[it] = mo[0];
+            syq[it] = S[K * K1 + K];
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {     // uniform trip count (shuffles)
+        const int i = r0 + g + it * (FT / 16);
         const bool row = i < r1;
         const int s = row ? ixs[i] : -1;
         const bool mine = row && s >= a.seg_lo && s < a.seg_hi;
         bool ok = false;
         double n = NAN, tb = 0.0, ty = 0.0, syy = NAN;
-        if (K < 16) {   // block-uniform: lane b owns column b (b <= K) of the month's S
-            // the month's n, Syy and this lane's S column are loaded together, clamped to a
-            // valid row (a loop of dependent loads waits one round trip per regressor)
-            const bool have = mine && i >= a.lag;
-            const int sr = have ? s - a.seg_lo : 0;
-            const double* mo = a.moments + ((int64_t)sr * a.nprob + p) * a.mom_stride;
-            const double* S = mo + 1 + K1;
-            const int bc = b <= K ? b : 0;
-            double sc[15];
-#pragma unroll
-            for (int r = 0; r < 15; ++r) sc[r] = S[(r < K ? r : 0) * K1 + bc];
-            const double n0 = mo[0], syy0 = S[K * K1 + K];
-            if (have) {
+        if (K < 16) {
+            if (mine && i >= a.lag) {
                 const double* c = rl + (i - a.lag - q0) * PM;
                 bool bad = false;
                 for (int q = 0; q <= K; ++q) bad |= isnan(c[q]);
-                n = n0;
+                n = n0q[it];
                 ok = !bad && n >= 2.0;
                 if (ok) {
-                    syy = syy0;
+                    syy = syq[it];
                     const double cb = b < K ? c[1 + b] : 0.0;
 #pragma unroll
                     for (int r = 0; r < 15; ++r) {
                         if (r < K) {
-                            const double v = sc[r] * c[1 + r];
+                            const double v = scq[it][r] * c[1 + r];
                             if (b < K) tb += v * cb;
                             else if (b == K) ty += v;
                         }
