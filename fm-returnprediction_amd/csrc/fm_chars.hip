@@ -136,11 +136,17 @@ __global__ __launch_bounds__(CT) void firm_chars_kernel(fm_chars_args a, int nee
 constexpr int ST_T = 256;            // threads
 constexpr int ST_R = 8;              // consecutive rows per thread
 constexpr int ST_ROWS = ST_T * ST_R; // rows per tile
-constexpr int ST_LU = 9;             // tile-load batch per thread (2048 + 251 halo rows = 9 per thread)
+constexpr int ST_HA = 128;           // halo rows are loaded from a 128-row aligned start
+#ifndef FM_STD_LP
+#define FM_STD_LP 4                  // load batches per thread (5: 105 VGPRs, one wave per SIMD less)
+#endif
 
 // LDS slot of halo element e: one pad slot per ST_R (the lanes of a wave read elements
 // ST_R apart; stride ST_R + 1 doubles puts 32 lanes on distinct bank pairs)
 __host__ __device__ __forceinline__ int spad(int e) { return e + e / ST_R; }
+// halo rows staged before the tile: the window's W - 1 rows rounded up to ST_HA, so every
+// wave loads 128 consecutive rows as 64 aligned 16-byte pairs
+__host__ __device__ __forceinline__ int st_halo(int W) { return ((W - 1 + ST_HA - 1) / ST_HA) * ST_HA; }
 
 // count / mean / M2 of the non-NaN observations of halo rows [a, b): two passes, no division
 // per observation
@@ -174,64 +180,110 @@ __device__ __forceinline__ RunStats range_stats(const double* xs, int a, int b) 
     return RunStats{c, mean, m2};
 }
 
+// bits 0..31 of x spread to the even bit positions of a 64-bit word (Morton interleave)
+__device__ __forceinline__ uint64_t spread_bits(uint32_t x32) {
+    uint64_t x = x32;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+
+// 64-bit lane value of lane - 1 (DPP wave_shr:1); lane 0 gets `first`
+__device__ __forceinline__ int64_t lane_prev_i64(int64_t v, int64_t first) {
+    const uint64_t u = (uint64_t)v, f = (uint64_t)first;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)f, (int)(uint32_t)u, 0x138, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(f >> 32), (int)(uint32_t)(u >> 32), 0x138,
+                                                               0xF, 0xF, false);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __restrict__ ids,
                                                            const double* __restrict__ x, int64_t n,
                                                            int W, int minp, double scale,
                                                            double* __restrict__ out) {
     extern __shared__ double sm[];
-    const int H = W - 1;
-    const int E = ST_ROWS + H;
+    const int H = W - 1;          // rows before a row that its window holds
+    const int HP = st_halo(W);    // halo rows staged (>= H, 128-aligned)
+    const int E = ST_ROWS + HP;   // staged rows (a multiple of 128)
     double* xs = sm;
-    // firm starts as a bit per halo row (one wave ballot per 64 rows) instead of an int64 id
-    // per row: 1 KB instead of 37 KB of LDS, so three workgroups share a CU
+    // firm starts as a bit per staged row (one wave ballot pair per 128 rows) instead of an
+    // int64 id per row: 1 KB instead of 37 KB of LDS, so several workgroups share a CU
     uint64_t* fb = (uint64_t*)(sm + spad(E) + 1);
-    const int nw = (E + 63) / 64;
+    const int nw = E / 64;
     const int64_t b = (int64_t)blockIdx.x * ST_ROWS;
-    // ST_LU rows per thread in flight: all loads of a batch are issued (clamped, so always
-    // in bounds) before the first LDS store waits on them
-    for (int e1 = threadIdx.x; e1 < E; e1 += ST_T * ST_LU) {
-        double v[ST_LU];
-        int64_t id[ST_LU], idp[ST_LU];
+    const int lane = (int)threadIdx.x & 63;
+    // Loads: lane l of a wave takes staged rows 2q, 2q + 1 (q = wave pair index) as ONE
+    // 16-byte load of x and one of ids (the rows' start is 128-aligned, hence even); the id
+    // of the row before the pair is the previous lane's second id (DPP wave shift), for
+    // lane 0 one scalar read -- no second pass over ids.  All batches are issued (clamped,
+    // in bounds) before the first LDS store waits on them.
+    constexpr int ST_LP = FM_STD_LP;   // pair batches per thread in flight (2,048 + 256 staged rows)
+    const int NP = E / 2;
+    for (int q1 = threadIdx.x; q1 < NP; q1 += ST_T * ST_LP) {
+        double2 v[ST_LP];
+        longlong2 id[ST_LP];
+        int64_t pid0[ST_LP];
 #pragma unroll
-        for (int k = 0; k < ST_LU; ++k) {
-            const int64_t r = b - H + e1 + k * ST_T;
-            const int64_t rc = r < 0 ? 0 : (r < n ? r : n - 1);
-            const int64_t rp = rc > 0 ? rc - 1 : 0;
-            v[k] = x[rc];
-            id[k] = ids[rc];
-            idp[k] = ids[rp];
+        for (int k = 0; k < ST_LP; ++k) {
+            const int q = q1 + k * ST_T;
+            const int64_t r = b - HP + 2 * (int64_t)q;   // even
+            if (r >= 0 && r + 1 < n) {
+                v[k] = *reinterpret_cast<const double2*>(x + r);
+                id[k] = *reinterpret_cast<const longlong2*>(ids + r);
+            } else {   // the array's edges (one wave per tile at most): two clamped reads
+                const int64_t r0 = r < 0 ? 0 : (r < n ? r : n - 1);
+                const int64_t r1 = r + 1 < 0 ? 0 : (r + 1 < n ? r + 1 : n - 1);
+                v[k] = make_double2(x[r0], x[r1]);
+                id[k] = make_longlong2(ids[r0], ids[r1]);
+            }
+            // the row before lane 0's pair (wave-uniform address: a scalar read)
+            const int64_t rl0 = b - HP + 2 * (int64_t)(q - lane);
+            pid0[k] = ids[rl0 >= 1 && rl0 - 1 < n ? rl0 - 1 : 0];
         }
 #pragma unroll
-        for (int k = 0; k < ST_LU; ++k) {
-            const int e = e1 + k * ST_T;   // a wave's 64 lanes hold 64 consecutive, 64-aligned rows
-            const int64_t r = b - H + e;
-            const bool in = r >= 0 && r < n;
-            const uint64_t starts = __ballot(in && (r == 0 || id[k] != idp[k]));
-            if (e < E) xs[spad(e)] = in ? nan_if_inf(v[k]) : (double)NAN;
-            if ((threadIdx.x & 63) == 0 && (e >> 6) < nw) fb[e >> 6] = starts;
+        for (int k = 0; k < ST_LP; ++k) {
+            const int q = q1 + k * ST_T;
+            if (q - lane >= NP) break;   // wave-uniform
+            const int e = 2 * q;
+            const int64_t r = b - HP + e;
+            const bool in0 = r >= 0 && r < n, in1 = r + 1 >= 0 && r + 1 < n;
+            const int64_t prev = lane_prev_i64(id[k].y, pid0[k]);
+            const uint64_t ev = __ballot(in0 && (r == 0 || id[k].x != prev));
+            const uint64_t od = __ballot(in1 && (r + 1 == 0 || id[k].y != id[k].x));
+            if (q < NP) {
+                xs[spad(e)] = in0 ? nan_if_inf(v[k].x) : (double)NAN;
+                xs[spad(e + 1)] = in1 ? nan_if_inf(v[k].y) : (double)NAN;
+            }
+            if (lane == 0) {   // rows 2q .. 2q + 127: fb words e / 64, e / 64 + 1
+                fb[e >> 6] = spread_bits((uint32_t)ev) | (spread_bits((uint32_t)od) << 1);
+                fb[(e >> 6) + 1] = spread_bits((uint32_t)(ev >> 32)) | (spread_bits((uint32_t)(od >> 32)) << 1);
+            }
         }
     }
     __syncthreads();
     // per-ST_R-row block statistics (count, mean, M2 about the block mean; two-pass) for this
-    // tile's own blocks and the nh whole blocks of the halo, so a first window adds ~W/16
+    // tile's own blocks and the nh whole blocks of the halo, so a first window adds ~W/8
     // block states instead of W observations
-    const int nh = H / ST_R;
+    const int nh = HP / ST_R;
     const int NB = ST_T + nh;
     double* bmean = (double*)(fb + nw);
     double* bm2 = bmean + NB;
     int* bcnt = (int*)(bm2 + NB);
     for (int s = threadIdx.x; s < NB; s += ST_T) {
-        const RunStats st = range_stats(xs, H + (s - nh) * ST_R, H + (s - nh + 1) * ST_R);
+        const RunStats st = range_stats(xs, HP + (s - nh) * ST_R, HP + (s - nh + 1) * ST_R);
         bmean[s] = st.mean;
         bm2[s] = st.m2;
         bcnt[s] = st.n;
     }
     __syncthreads();
     const int t = threadIdx.x;
-    const int e0 = H + t * ST_R;   // halo index of this thread's first row
+    const int e0 = HP + t * ST_R;   // staged index of this thread's first row
     const int64_t i0 = b + t * ST_R;
     if (i0 >= n) return;
-    // first window: halo rows [lo, e0], lo = max(e0 - H, the firm's first row): the highest
+    // first window: staged rows [lo, e0], lo = max(e0 - H, the firm's first row): the highest
     // firm-start bit at or below e0 (fs = -1 when the firm starts before the window)
     const int lo0 = e0 - H;
     int fs = -1;
@@ -243,7 +295,7 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     }
     const int lo = fs > lo0 ? fs : lo0;
     // [lo, e0] = a head range, whole blocks jlo..t-1 (all rows inside the firm), row e0
-    const int jlo = lo >= H ? (lo - H + ST_R - 1) / ST_R : -((H - lo) / ST_R);
+    const int jlo = lo >= HP ? (lo - HP + ST_R - 1) / ST_R : -((HP - lo) / ST_R);
     // window state as count and sums of (x - K), (x - K)^2 about K = a block mean next to
     // the window end: each block / range state (n, mean, M2) adds n*d and M2 + n*d^2 with
     // d = mean - K (exact algebra, no division, four independent chains)
@@ -265,7 +317,7 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     if (jlo >= t) {
         add_state(range_stats(xs, lo, e0 + 1));
     } else {
-        add_state(range_stats(xs, lo, H + jlo * ST_R));
+        add_state(range_stats(xs, lo, HP + jlo * ST_R));
         int c4[4] = {0, 0, 0, 0};
         double a4[4] = {0.0, 0.0, 0.0, 0.0}, q4[4] = {0.0, 0.0, 0.0, 0.0};
         int j = jlo;
@@ -303,9 +355,9 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
         ++run;
     }
     const int need = minp > 2 ? minp : 2;
+    double res[ST_R];
+#pragma unroll
     for (int r = 0; r < ST_R; ++r) {
-        const int64_t i = i0 + r;
-        if (i >= n) break;
         const int e = e0 + r;
         if (r > 0) {
             if ((fb[e >> 6] >> (e & 63)) & 1ull) {   // a new firm starts here
@@ -339,17 +391,27 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
                 last = v;
             }
         }
-        double res = NAN;
+        double rv = NAN;
         if (cnt >= need) {
             if (run >= cnt) {
-                res = 0.0;   // pandas: every observation in the window is the same value
+                rv = 0.0;   // pandas: every observation in the window is the same value
             } else {
                 const double c = (double)cnt;
                 const double var = (s2 * c - s1 * s1) / (c * (c - 1.0));
-                res = sqrt(var > 0.0 ? var : 0.0) * scale;
+                rv = sqrt(var > 0.0 ? var : 0.0) * scale;
             }
         }
-        out[i] = res;
+        res[r] = rv;
+    }
+    // 16-byte stores of row pairs (i0 is even); the array's last odd row alone
+    if (i0 + ST_R <= n) {
+#pragma unroll
+        for (int r = 0; r < ST_R; r += 2)
+            *reinterpret_cast<double2*>(out + i0 + r) = make_double2(res[r], res[r + 1]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < ST_R; ++r)
+            if (i0 + r < n) out[i0 + r] = res[r];
     }
 }
 
@@ -402,8 +464,8 @@ extern "C" int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, in
     FM_REQUIRE(ids && x && out, "fm_rolling_std: null pointer");
     FM_REQUIRE(window >= 1 && window <= 4096, "fm_rolling_std: window must be 1..4096");
     FM_REQUIRE(min_periods >= 1 && min_periods <= window, "fm_rolling_std: min_periods must be 1..window");
-    const int E = ST_ROWS + window - 1;
-    const int nb = ST_T + (window - 1) / ST_R;
+    const int E = ST_ROWS + st_halo(window);
+    const int nb = ST_T + st_halo(window) / ST_R;
     const size_t lds = (size_t)(spad(E) + 1) * 8 + (size_t)((E + 63) / 64) * 8 + (size_t)nb * (8 * 2 + 4);
     FM_REQUIRE(lds <= 160 * 1024, "fm_rolling_std: window too large for LDS");
     const int64_t blocks = (n + ST_ROWS - 1) / ST_ROWS;
