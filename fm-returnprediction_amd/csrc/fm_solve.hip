@@ -507,7 +507,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         double sii = 0.0, sxy = 0.0, gdiag = 0.0;
         static_for<0, G16>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            if (i == j) gdiag = G[j];
+            gdiag = i == j ? G[j] : gdiag;   // selects, not conditional stores (see below)
             if constexpr (j + 1 < G16) {
                 if (j > kw) {   // wave-uniform: past every problem's last column
                     row[j] = 0.0;
@@ -516,8 +516,11 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                 const double g0j = rowbc<0>(G[j + 1]);   // G[0][j+1]
                 const double v = srow && j < K1 ? G[j + 1] - G[0] * g0j * ninv : 0.0;
                 row[j] = v;
-                if (i == j + 1) sii = v;
-                if (j == K) sxy = v;
+                // conditional assignments to these per-lane scalars were merged by the
+                // compiler into a store through a selected address, which kept them in
+                // scratch memory; plain selects keep them in registers
+                sii = i == j + 1 ? v : sii;
+                sxy = j == K ? v : sxy;
             } else {
                 row[j] = 0.0;
             }
@@ -578,10 +581,10 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                 constexpr int j = decltype(jc)::value;
                 if (j > kw) return;   // wave-uniform
                 const double sj = rowbc<k + 1>(row[j]) * rinv;   // L[j][k] = S(k)[k][j] / lkk
-                if (go && j <= K) row[j] -= lik * sj;
+                row[j] = go && j <= K ? row[j] - lik * sj : row[j];
             });
-            if (go) row[k] = i == k + 1 ? lkk : lik;
-            if (i == k + 1) dinv = rinv;
+            row[k] = go ? (i == k + 1 ? lkk : lik) : row[k];
+            dinv = i == k + 1 ? rinv : dinv;
         });
         // lanes of a live, unskipped problem with a collapsed pivot: rank deficient
         const bool rank_def = act0 && !ok;
