@@ -557,13 +557,290 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
     }
 }
 
+// ---- High-key tail kernel (the default for tail ranks without a row mask).
+//
+// The FP64 kernel above holds a unit's values in 80 VGPRs per thread, so only two 512-thread
+// workgroups fit a CU and the chip idles its HBM while both compute.  The tails need far less:
+// every step before the final candidate sort works on the HIGH 32 bits of the values' order
+// keys (thread extrema, per-wave thresholds, ballot counts, compaction), and only the
+// candidates' full values are gathered back from memory (a few hundred per unit).  40 VGPRs
+// of keys per thread: three workgroups per CU.  The grid is persistent: once a unit's
+// candidates are compacted its key registers are dead, so the next unit's loads are issued
+// right behind the candidate gather and fly during the sort and merge (measured on 1,000 x
+// 20,000 x 15: up to the compaction 0.42 ms, the gather +0.12 ms, sort +0.07, merge +0.05
+// when each unit waited for its own gather).
+//
+// hkey: the dkey high word shifted so that -inf -> 0 and +inf -> HK_MAX, order-preserving over
+// non-NaN values, and EVERY NaN lands above HK_MAX (positive NaNs above +inf, negative NaNs
+// wrap past the top).  The one thing a high word cannot tell is +-inf from a NaN whose payload
+// is all in the low word (high word 0x7FF00000 / 0xFFF00000): units holding either key
+// (thread min 0 / thread max HK_MAX) are marked and redone by the exact streaming kernel.
+#ifndef FM_HK_RIDE
+#define FM_HK_RIDE 1   // a universe rides the high-key kernel's launch (one more grid column)
+#endif
+#ifndef FM_AB_NOFB
+#define FM_AB_NOFB 0   // timing / probe builds only: no fallback launch after the long kernel
+#endif
+#ifndef FM_AB_LONG_F64
+#define FM_AB_LONG_F64 0   // timing builds only: 1 = tails on the FP64-register kernel above
+#endif
+constexpr uint32_t HK_MAX = 0xFFE00001u;
+constexpr uint32_t HK_NONE = 0xFFFFFFFFu;   // thread / threshold sentinel (no valid value)
+__device__ __forceinline__ uint32_t hkey(uint32_t hi) {
+    const uint32_t m = (uint32_t)((int32_t)hi >> 31) | 0x80000000u;
+    return (hi ^ m) - 0x000FFFFFu;
+}
+
+struct LongHkSmem {
+    uint64_t ck[2 * LCAP];       // candidate keys: lower tail, then upper tail at LCAP
+    int cidx[2 * LCAP];          // candidate rows (compaction), same layout
+    SelSmemT<LNW> hs;            // block reductions (and the riding universe's hist_select)
+    uint32_t tw[2][LNW];
+    int tot[2][LNW];
+    int wc[2][LNW];
+    uint64_t res[4];
+};
+
+// The high words of a unit into hk (raw; hkey is applied by the unit's own pass): buffer
+// loads, one descriptor per slot of LT rows (scalar), the lane's byte offset the only VGPR;
+// rows past the month end read 0 through the descriptor's range check (masked later).
+template <int VPT>
+__device__ __forceinline__ void hk_load(const double* col, int L, uint32_t (&hk)[VPT]) {
+    const uint32_t lb = (uint32_t)threadIdx.x * 8u + 4u;   // little-endian: byte 4 = high word
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const int rem = L - v * LT;   // rows from this slot's first row to the month end
+        const int nrec = rem > 0 ? (rem < LT ? rem : LT) * 8 : 0;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(col + (rem > 0 ? v * LT : 0)), 0, nrec,
+                                                          0x00020000);
+        hk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb, 0, 0);
+    }
+}
+
+// One (month, column) unit whose raw high words are in hk.
+template <int VPT>
+__device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t (&hk)[VPT], LongHkSmem& sm) {
+    const int tid = (int)threadIdx.x, lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
+    const int64_t o = (int64_t)c * a.nseg + s;
+    const int64_t r0 = a.seg_off[s];
+    const int L = (int)(a.seg_off[s + 1] - r0);
+    const double* col = a.cols + (int64_t)c * a.col_stride + r0;
+    // rows past the month end (read as 0 by the range check) -> HK_NONE; straight-line (a
+    // scalar branch per slot split the block and pushed keys into scratch)
+    const int lim = L - tid;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) hk[v] = v * LT < lim ? hkey(hk[v]) : HK_NONE;
+    // count of valid values (ballots: scalar counts), thread min key and max key (NaN keys are
+    // above HK_MAX for the min; +0x1FFFFE moves them below every valid key for the max)
+    int cw = 0;
+    uint32_t kmn = HK_NONE, kmx2 = 0;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        cw += (int)__popcll(__ballot(hk[v] <= HK_MAX));
+        kmn = hk[v] < kmn ? hk[v] : kmn;
+        const uint32_t k2 = hk[v] + 0x1FFFFEu;
+        kmx2 = k2 > kmx2 ? k2 : kmx2;
+        // in order: otherwise the ballot masks are hoisted (SGPR spills) and every k2 kept
+        asm volatile("" : "+s"(cw), "+v"(kmn), "+v"(kmx2));
+    }
+    const bool tvalid = kmn <= HK_MAX;   // this thread holds a valid value
+    const uint32_t kmx = kmx2 - 0x1FFFFEu;
+    const uint32_t ua = tvalid ? kmn : HK_NONE;            // lower-tail thread key
+    const uint32_t ub = tvalid ? HK_MAX - kmx : HK_NONE;   // upper-tail thread key
+    const bool amb = tvalid && (kmn == 0u || kmx == HK_MAX);
+    if (tid < 2 * LNW) sm.tot[tid / LNW][tid % LNW] = 0;
+    // valid count (low 16 bits per wave: <= 64 * VPT) and ambiguous-key threads, one reduction
+    const int packed = block_sum<LNW>(lane == 0 ? cw + ((int)__popcll(__ballot(amb)) << 16) : 0, sm.hs.ints);
+    const int n = packed & 0xFFFF;
+    double lo = NAN, hi = NAN;
+    bool ok = (packed >> 16) == 0;
+    // phases: thresholds + compaction (cand), then ONE site that gathers the candidates and
+    // issues the next unit's loads (every path reaches it), then the sort / merge
+    bool cand = false;
+    int i0 = 0, j0 = 0, i1 = 0, j1 = 0, clo = 0, chi = 0;
+    double g0 = 0.0, g1 = 0.0;
+    if (ok && n >= a.min_count && n > 0) {   // block-uniform
+        qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
+        qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
+        const int kl = j0, ku = n - 1 - i1;        // largest ranks needed from either end
+        const int ql = kl / LNW + 1, qu = ku / LNW + 1;
+        ok = ql <= WAVE && qu <= WAVE;
+        uint32_t tl = HK_NONE, tu = HK_NONE;
+        if (ok) {
+            uint32_t ha[1] = {ua}, hb[1] = {ub};
+            wave_sort32<1>(ha);
+            wave_sort32<1>(hb);
+            if (lane == 0) {
+                sm.tw[0][w] = (uint32_t)__builtin_amdgcn_readlane((int)ha[0], ql - 1);
+                sm.tw[1][w] = (uint32_t)__builtin_amdgcn_readlane((int)hb[0], qu - 1);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < LNW; ++q) {
+                const uint32_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
+                const int ca = (int)__popcll(__ballot(ua != HK_NONE && ua <= Ta));
+                const int cb = (int)__popcll(__ballot(ub != HK_NONE && ub <= Tb));
+                if (lane == 0) {
+                    atomicAdd(&sm.tot[0][q], ca);
+                    atomicAdd(&sm.tot[1][q], cb);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < LNW; ++q) {
+                const uint32_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
+                if (Ta != HK_NONE && sm.tot[0][q] >= kl + 1 && Ta < tl) tl = Ta;
+                if (Tb != HK_NONE && sm.tot[1][q] >= ku + 1 && Tb < tu) tu = Tb;
+            }
+            ok = tl != HK_NONE && tu != HK_NONE;
+        }
+        if (ok) {
+            // candidates: key <= tl (a prefix of the sorted values) / HK_MAX - key <= tu (a
+            // suffix); NaN keys fail both (the subtraction wraps them above every tu)
+            int wl = 0, wh = 0;
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+                uint32_t k = hk[v];
+                asm volatile("" : "+v"(k));   // no values derived in the count loop kept for here
+                wl += (int)__popcll(__ballot(k <= tl));
+                wh += (int)__popcll(__ballot(HK_MAX - k <= tu));
+                asm volatile("" : "+s"(wl), "+s"(wh));   // counts in order (no spilled masks)
+            }
+            if (lane == 0) {
+                sm.wc[0][w] = wl;
+                sm.wc[1][w] = wh;
+            }
+            __syncthreads();
+            int ol = 0, oh = LCAP;
+#pragma unroll
+            for (int q = 0; q < LNW; ++q) {
+                const int a0 = sm.wc[0][q], a1 = sm.wc[1][q];
+                ol += q < w ? a0 : 0;
+                oh += q < w ? a1 : 0;
+                clo += a0;
+                chi += a1;
+            }
+            ok = clo <= LCAP && chi <= LCAP && clo + chi <= n && clo > kl && chi > ku;
+            if (ok) {
+#pragma unroll
+                for (int v = 0; v < VPT; ++v) {
+                    uint32_t k = hk[v];
+                    asm volatile("" : "+v"(k));
+                    const bool bl = k <= tl, bh = HK_MAX - k <= tu;
+                    const uint64_t ml = __ballot(bl), mh = __ballot(bh);
+                    const int row = tid + v * LT;
+                    if (ml) {   // wave-uniform: most value slots hold no candidate
+                        if (bl) sm.cidx[ol + mask_rank(ml)] = row;
+                        ol += (int)__popcll(ml);
+                    }
+                    if (mh) {
+                        if (bh) sm.cidx[oh + mask_rank(mh)] = row;
+                        oh += (int)__popcll(mh);
+                    }
+                }
+                __syncthreads();
+                cand = true;
+            }
+        }
+    }
+    if (cand) {   // block-uniform
+        // gather the candidates' full values (a few hundred rows of the unit just read); wave
+        // w sorts run w of each tail (64 keys; the upper tail on complemented keys), then every
+        // candidate's merged rank = its run position + the entries of the other runs before it.
+        // (Ordering the candidates by (high key, row) first and gathering only the tie groups at
+        // the target ranks measured slower: 0.91-1.0 vs 0.66 ms on 1,000 x 20,000 x 15.)
+        const int e = w * WAVE + lane;
+        const int nrl = __builtin_amdgcn_readfirstlane((clo + WAVE - 1) / WAVE);
+        const int nru = __builtin_amdgcn_readfirstlane((chi + WAVE - 1) / WAVE);
+        const int rl = e < clo ? sm.cidx[e] : 0, ru = e < chi ? sm.cidx[LCAP + e] : 0;
+        const double xl = col[rl], xu = col[ru];
+        uint64_t ka[1] = {e < clo ? dkey(xl) : SENT};
+        uint64_t kb[1] = {e < chi ? ~dkey(xu) : SENT};
+        if (w < nrl) wave_sort<1>(ka);
+        if (w < nru) wave_sort<1>(kb);
+        sm.ck[e] = ka[0];
+        sm.ck[LCAP + e] = kb[0];
+        if (tid < 4) sm.res[tid] = SENT;
+        __syncthreads();
+        if (ka[0] != SENT) {
+            int r = lane;
+            for (int u = 0; u < nrl; ++u)
+                if (u != w) r += merge_count(sm.ck + u * WAVE, ka[0], u < w);
+            if (r == i0) sm.res[0] = ka[0];
+            if (r == j0) sm.res[1] = ka[0];
+        }
+        if (kb[0] != SENT) {
+            int r = lane;
+            for (int u = 0; u < nru; ++u)
+                if (u != w) r += merge_count(sm.ck + LCAP + u * WAVE, kb[0], u < w);
+            if (r == n - 1 - i1) sm.res[2] = ~kb[0];
+            if (r == n - 1 - j1) sm.res[3] = ~kb[0];
+        }
+        __syncthreads();
+        lo = qlerp(kval(sm.res[0]), kval(sm.res[1]), g0, a.lerp_mode);
+        hi = qlerp(kval(sm.res[2]), kval(sm.res[3]), g1, a.lerp_mode);
+    }
+    if (!ok) {   // redone by select_stream_kernel<true>
+        if (tid == 0) a.nvalid[o] = -1;
+    } else {
+        if (a.center != nullptr) {
+            // Gram pivot: the midpoint of the cuts, else of the finite range (no +-inf here:
+            // those units were marked above), else 0 -- the range re-read in full (rare: too
+            // few values)
+            double cen = 0.5 * (lo + hi);
+            if (!isfinite(cen)) {   // block-uniform
+                uint64_t m1 = SENT, m2 = SENT;
+                for (int r = tid; r < L; r += LT) {
+                    const double x = col[r];
+                    if (isfinite(x)) {
+                        m1 = dkey(x) < m1 ? dkey(x) : m1;
+                        m2 = ~dkey(x) < m2 ? ~dkey(x) : m2;
+                    }
+                }
+                m1 = block_min_u64<LNW>(m1, sm.hs.u64s);
+                m2 = block_min_u64<LNW>(m2, sm.hs.u64s + LNW);
+                cen = m1 == SENT || m2 == SENT ? 0.0 : 0.5 * (kval(m1) + kval(~m2));
+                if (!isfinite(cen)) cen = 0.0;
+            }
+            if (tid == 0) a.center[o] = cen;
+        }
+        if (tid == 0) {
+            a.lo[o] = lo;
+            a.hi[o] = hi;
+            a.nvalid[o] = n;
+        }
+    }
+    __syncthreads();   // the LDS is rewritten by the next unit
+}
+
+// One unit per workgroup (grid months x (columns [+ 1 riding universe column])): 80 VGPRs, three
+// workgroups per CU; the hardware refills a CU slot as a unit ends.  (A persistent grid with
+// the next unit's loads in flight during the sort and merge measured slower: 0.75-0.79 vs
+// 0.66 ms on the 1,000 x 20,000 x 15 panel, two workgroups per CU at 128 VGPRs.)
+template <int VPT>
+__global__ __launch_bounds__(LT, 6) void select_long_hk_kernel(SelArgs a) {
+    __shared__ LongHkSmem sm;
+    const int s = blockIdx.x, c = blockIdx.y;
+    if (FM_HK_RIDE && c == a.ncols) {   // fm_select_universe: the month's NYSE breakpoints + levels
+        universe_month_wg<LNW, HB, HCAP>(a, s, sm.hs);
+        return;
+    }
+    uint32_t hk[VPT];
+    hk_load<VPT>(a.cols + (int64_t)c * a.col_stride + a.seg_off[s], (int)(a.seg_off[s + 1] - a.seg_off[s]), hk);
+    hk_unit<VPT>(a, s, c, hk, sm);
+}
+
+
 template <int VPT>
 void launch_long(const SelArgs& a, hipStream_t st, bool mid) {
     if (mid)
         hipLaunchKernelGGL((select_long_kernel<VPT, true>), dim3(a.nseg, a.ncols), dim3(LT), 0, st, a);
-    else   // with a universe (a.ume), one more grid column: its months' NYSE breakpoints
+    else if (FM_AB_LONG_F64 || FM_AB_LONG != 0)   // with a universe (a.ume), one more grid column
         hipLaunchKernelGGL((select_long_kernel<VPT, false>), dim3(a.nseg, a.ncols + (a.ume ? 1 : 0)), dim3(LT), 0,
                            st, a);
+    else   // with a universe (a.ume), one more grid column: its months' NYSE breakpoints
+        hipLaunchKernelGGL((select_long_hk_kernel<VPT>), dim3(a.nseg, a.ncols + (a.ume ? 1 : 0)), dim3(LT), 0, st, a);
 }
 
 // the tail thresholds serve ranks < 512 from either end; row masks and middle ranks take the
@@ -1200,7 +1477,8 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
     // need the histogram (MID) kernel; on every other path it is launched first, on its own
     // (riding the two-wave kernel's persistent workgroups measured slower for short months:
     // 118 vs 83 + 23 us on the bench panel, profiles/r04/v2_kbench_fused_universe.log)
-    const bool ride = u != nullptr && long_path && !long_is_mid(a, max_seg_len);
+    const bool ride = u != nullptr && long_path && !long_is_mid(a, max_seg_len) &&
+                      (FM_HK_RIDE || FM_AB_LONG_F64 || FM_AB_LONG != 0);
     if (u != nullptr && !ride) {
         const int rcu = universe_separately(x, u, stream);
         if (rcu != FM_OK) return rcu;
@@ -1213,7 +1491,7 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
         const int rc = launch_select_long(al, max_seg_len, st);
         if (rc != FM_OK) return rc;
         FM_CHECK_LAUNCH("fm_select_cuts(long)");
-        hipLaunchKernelGGL(select_stream_kernel<true>, dim3(256), dim3(ST), 0, st, a);
+        if (!FM_AB_NOFB) hipLaunchKernelGGL(select_stream_kernel<true>, dim3(256), dim3(ST), 0, st, a);
         FM_CHECK_LAUNCH("fm_select_cuts(long fallback)");
         // the level bytes by a streaming launch: writing them from the select kernel (a
         // re-read of the unmasked column, or unmasked registers + mask bits) measured no
