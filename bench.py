@@ -370,13 +370,7 @@ def firm_chars_stage(args, E):
     out = torch.empty_like(x)
     E.rolling_std(dids, x, out=out)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        E.rolling_std(dids, x, out=out)
-    e1.record()
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / 10
+    ms = E.time_launch("fm_rolling_std", 20)
     drows = int(x.shape[0])
     gbs = drows * 24 / (ms * 1e-3) / 1e9
     res["daily_std"] = {"rows": drows, "ms": ms, "rows_per_s": drows / (ms * 1e-3),

@@ -926,8 +926,9 @@ def rolling_std(ids, x, window=252, min_periods=100, scale=252 ** 0.5, out=None)
         out = torch.empty(n, dtype=torch.float64, device=x.device)
     if out.dtype != torch.float64 or out.shape != (n,) or not out.is_contiguous():
         raise ValueError("rolling_std: out must be a contiguous float64 [n] tensor")
-    _kcall("fm_rolling_std", "fm_rolling_std", ids.data_ptr(), x.data_ptr(), n, int(window),
-           int(min_periods), float(scale), out.data_ptr(), _stream())
+    args = (ids.data_ptr(), x.data_ptr(), n, int(window), int(min_periods), float(scale), out.data_ptr())
+    _kcall("fm_rolling_std", "fm_rolling_std", *args, _stream())
+    LAST_LAUNCH["fm_rolling_std"] = ("fm_rolling_std", None, ((ids, x, out), args))
     return out
 
 
