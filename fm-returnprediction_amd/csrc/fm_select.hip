@@ -570,6 +570,9 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
 // 20,000 x 15: up to the compaction 0.42 ms, the gather +0.12 ms, sort +0.07, merge +0.05
 // when each unit waited for its own gather).
 //
+// (Thresholds from each thread's two smallest / largest keys instead of one measured slower:
+// 0.72 vs 0.64 ms -- three more wave sorts per tail cost more than the fewer candidates save.)
+//
 // hkey: the dkey high word shifted so that -inf -> 0 and +inf -> HK_MAX, order-preserving over
 // non-NaN values, and EVERY NaN lands above HK_MAX (positive NaNs above +inf, negative NaNs
 // wrap past the top).  The one thing a high word cannot tell is +-inf from a NaN whose payload
@@ -637,10 +640,10 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
     uint32_t kmn = HK_NONE, kmx2 = 0;
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
-        cw += (int)__popcll(__ballot(hk[v] <= HK_MAX));
-        kmn = hk[v] < kmn ? hk[v] : kmn;
-        const uint32_t k2 = hk[v] + 0x1FFFFEu;
-        kmx2 = k2 > kmx2 ? k2 : kmx2;
+        const uint32_t k = hk[v];
+        cw += (int)__popcll(__ballot(k <= HK_MAX));
+        kmn = min(kmn, k);
+        kmx2 = max(kmx2, k + 0x1FFFFEu);
         // in order: otherwise the ballot masks are hoisted (SGPR spills) and every k2 kept
         asm volatile("" : "+s"(cw), "+v"(kmn), "+v"(kmx2));
     }
@@ -651,7 +654,9 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
     const bool amb = tvalid && (kmn == 0u || kmx == HK_MAX);
     if (tid < 2 * LNW) sm.tot[tid / LNW][tid % LNW] = 0;
     // valid count (low 16 bits per wave: <= 64 * VPT) and ambiguous-key threads, one reduction
-    const int packed = block_sum<LNW>(lane == 0 ? cw + ((int)__popcll(__ballot(amb)) << 16) : 0, sm.hs.ints);
+    // (the ballot outside the lane-0 select: inside it, it would see lane 0's flag only)
+    const int ambw = (int)__popcll(__ballot(amb));
+    const int packed = block_sum<LNW>(lane == 0 ? cw + (ambw << 16) : 0, sm.hs.ints);
     const int n = packed & 0xFFFF;
     double lo = NAN, hi = NAN;
     bool ok = (packed >> 16) == 0;

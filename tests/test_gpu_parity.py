@@ -220,6 +220,61 @@ def test_long_month_register_select_bit_exact(E, maxlen):
             assert _same([lo[t]], [ra]) and _same([hi[t]], [rb]), (qa, qb, t, len(v), lo[t], ra, hi[t], rb)
 
 
+def _payload_nan(sign, n):
+    """n NaNs whose payload sits entirely in the LOW 32 bits (high word 0x7FF00000 /
+    0xFFF00000, the same high word as +-inf)."""
+    bits = np.full(n, (0xFFF00000 if sign < 0 else 0x7FF00000) << 32, dtype=np.uint64)
+    bits |= np.arange(1, n + 1, dtype=np.uint64)
+    return bits.view(np.float64)
+
+
+@pytest.mark.parametrize("maxlen", [9000, 20000])
+def test_long_month_high_key_edge_cases(E, maxlen):
+    """The long-month kernel orders values by the high 32 bits of their keys until the final
+    candidate sort.  Units whose high words cannot tell +-inf from a NaN (payload only in the
+    low word) are redone by the streaming kernel: bit-exact against np.percentile over the
+    non-NaN values with such NaNs, with +-inf in the tails, with both, with values that share
+    high words across the cut ranks (differing only in the low word), and with the cut ranks
+    inside a long run of equal high words."""
+    rng = np.random.default_rng(maxlen + 7)
+    n = maxlen
+    segs = []
+    x = rng.standard_normal(n)
+    x[rng.choice(n, 40, replace=False)] = _payload_nan(1, 40)
+    x[rng.choice(n, 40, replace=False)] = _payload_nan(-1, 40)
+    segs.append(x)                                   # low-payload NaNs, no infinities
+    x = rng.standard_normal(n)
+    x[rng.choice(n, 30, replace=False)] = np.inf
+    x[rng.choice(n, 30, replace=False)] = -np.inf
+    segs.append(x)                                   # +-inf inside both tails
+    x = rng.standard_normal(n)
+    x[rng.choice(n, 5, replace=False)] = np.inf
+    x[rng.choice(n, 25, replace=False)] = _payload_nan(1, 25)
+    segs.append(x)                                   # both
+    base = 1.0 + rng.integers(0, 2 ** 20, n).astype(np.uint64)   # low-word-only differences
+    segs.append((np.float64(3.0).view(np.uint64) + base).view(np.float64) * np.where(rng.random(n) < 0.5, 1, -1))
+    x = rng.standard_normal(n)
+    k = n // 20                                      # 5% of rows: one high word at each end
+    x[:k] = (np.float64(-7.0).view(np.uint64) + np.arange(k, dtype=np.uint64)).view(np.float64)
+    x[-k:] = (np.float64(7.0).view(np.uint64) + np.arange(k, dtype=np.uint64)).view(np.float64)
+    segs.append(rng.permutation(x))
+    segs.append(rng.standard_normal(6500))
+    vals = np.concatenate(segs)
+    labels = np.repeat(np.arange(len(segs)), [len(s) for s in segs])
+    panel = E.panel_from_arrays([vals], ["v"], labels)
+    assert panel.max_seg_len == maxlen
+    for qa, qb in ((1, 99), (0, 100), (2, 98)):
+        cuts = E.select_cuts(panel, qa / 100, qb / 100, 1, E.LERP_NUMPY, center=True)
+        lo, hi = cuts.lo.cpu().numpy()[0], cuts.hi.cpu().numpy()[0]
+        nv = cuts.nvalid.cpu().numpy()[0]
+        for t, s in enumerate(segs):
+            v = s[~np.isnan(s)]
+            assert nv[t] == len(v), t
+            with np.errstate(invalid="ignore"):
+                ra, rb = np.percentile(v, qa), np.percentile(v, qb)
+            assert _same([lo[t]], [ra]) and _same([hi[t]], [rb]), (qa, qb, t, lo[t], ra, hi[t], rb)
+
+
 def test_masked_middle_quantiles_hist_select(E):
     """NYSE-style row-masked middle quantiles (pandas lerp) through the workgroup path's
     adaptive histogram select, incl. clustered keys that need the refinement levels."""
