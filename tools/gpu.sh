@@ -21,6 +21,7 @@ for s in "$@"; do
     split)   specs+=("split:::300:::python tools/split_scan.py");;
     rehearse) specs+=("rehearse:::400:::python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --one-device --c5-months 400 --months 300");;
     kbench)  specs+=("kbench:::300:::python tools/kbench.py $KB_LIBS");;
+    slab)    specs+=("slab:::300:::python tools/slab_probe.py");;
     selbench) specs+=("selbench:::300:::python tools/selbench.py $KB_LIBS");;
     stdbench) specs+=("stdbench:::300:::python tools/stdbench.py $KB_LIBS");;
     kstats)  specs+=("kstats:::500:::$PROF --kernel-trace --stats -d $R/gpurun_out/kt -o kt --output-format csv -- python3 $R/bench.py --no-cpu --no-chars --steps 10 $BENCH_ARGS");;
