@@ -133,8 +133,16 @@ __global__ __launch_bounds__(CT) void firm_chars_kernel(fm_chars_args a, int nee
 }
 
 // ---- rolling std --------------------------------------------------------------------------
-constexpr int ST_T = 256;            // threads
-constexpr int ST_R = 8;              // consecutive rows per thread
+// tile shape (timing builds may override): 256 x 8 measured best -- 512 x 8 0.116, 256 x 16
+// 0.119, 512 x 4 0.179, 1024 x 4 0.205 vs 0.111 ms (profiles/r04/v11_stdbench_tile_sweep.log)
+#ifndef FM_STD_T
+#define FM_STD_T 256
+#endif
+#ifndef FM_STD_R
+#define FM_STD_R 8
+#endif
+constexpr int ST_T = FM_STD_T;       // threads
+constexpr int ST_R = FM_STD_R;       // consecutive rows per thread
 constexpr int ST_ROWS = ST_T * ST_R; // rows per tile
 constexpr int ST_HA = 128;           // halo rows are loaded from a 128-row aligned start
 #ifndef FM_STD_LP
