@@ -41,9 +41,12 @@ C5_MONTHS, C5_FIRMS, C5_SEED = 12500, 20000, 20150101   # per rank (C5 = 100,000
 B_ROW = 15 * 8 + 8 + 1   # input bytes of a firm-month row: 15 FP64 columns, me, the NYSE flag
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment, N > 1 starts "
+                         "N worker processes itself through torch.distributed.run (default: "
+                         "WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("headline", "c5"), default=None,
@@ -66,7 +69,64 @@ def parse():
                     help="N>1 process group backend (nccl = RCCL; gloo only to rehearse on one GPU)")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 (with --dist-backend gloo)")
-    return ap.parse_args()
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="test aid: start the ranks as for --gpus N, join a gloo group on the CPU, "
+                         "print rank 0's {n_gpus, dist_world} and exit (no GPU call)")
+    return ap.parse_args(argv)
+
+
+class LaunchError(SystemExit):
+    """--gpus disagrees with the rank count the launcher gave this process."""
+
+    def __init__(self, msg):
+        print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+        super().__init__(2)
+
+
+def launch_plan(gpus, env, argv, port=None):
+    """How `bench.py --gpus N` gets N ranks (decided before anything touches the GPU).
+
+    * Under a launcher (WORLD_SIZE set, e.g. the driver's torch.distributed.run line), this
+      process IS one rank: returns None, and a --gpus that differs from WORLD_SIZE is an
+      error (LaunchError, exit 2), never a silent one-rank run.
+    * Without one and N > 1: the command that starts N fresh worker processes, one per GPU,
+      through torch.distributed.run on 127.0.0.1 with the same arguments; this process only
+      waits for them (rank 0 prints the JSON line).
+    * Otherwise (N = 1): None, one in-process rank."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        ws = int(ws)
+        if gpus is not None and gpus != ws:
+            raise LaunchError(f"--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks")
+        return None
+    if gpus is None or gpus <= 1:
+        if gpus is not None and gpus < 1:
+            raise LaunchError(f"--gpus {gpus}: need at least one GPU")
+        return None
+    if port is None:
+        port = env.get("MASTER_PORT") or _free_port()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _launch_probe(world):
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    out = {"n_gpus": world, "dist_backend": dist.get_backend() if world > 1 else None,
+           "dist_world": dist.get_world_size() if world > 1 else 1,
+           "rank": int(os.environ.get("RANK", "0"))}
+    if out["rank"] == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def timed_steps(step, steps, warmup, graph, world, dev):
@@ -138,8 +198,17 @@ def kernel_roofline(step, panel, E, steps):
 
 
 def main():
-    args = parse()
+    argv = sys.argv[1:]
+    args = parse(argv)
+    cmd = launch_plan(args.gpus, os.environ, argv)
+    if cmd is not None:
+        # N worker ranks as child processes (this process never touched the GPU); their
+        # stdout is ours, rank 0 prints the line; exit with the launcher's status
+        import subprocess
+        sys.exit(subprocess.run(cmd).returncode)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.launch_probe:
+        return _launch_probe(world)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.one_device:
@@ -184,6 +253,8 @@ def main():
         "value": rows_local * world * args.steps / dt,
         "unit": "firm-month rows/s",
         "n_gpus": world,
+        "dist_backend": torch.distributed.get_backend() if world > 1 else None,
+        "dist_world": torch.distributed.get_world_size() if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_step,

@@ -139,3 +139,62 @@ def test_combine_predictive_real_shard_outputs(world):
         assert p.exitcode == 0
     for rank, same_st, same_pred in out:
         assert same_st and same_pred, rank
+
+
+# ------------------------------------------------------------ bench.py --gpus N launcher
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_bench_launch_plan():
+    """--gpus N without a launcher spawns N ranks through torch.distributed.run on
+    127.0.0.1; under a launcher (WORLD_SIZE set) the process is one rank; a disagreeing
+    --gpus exits non-zero instead of measuring one rank."""
+    B = _bench()
+    argv = ["--gpus", "8", "--steps", "5"]
+    cmd = B.launch_plan(8, {}, argv, port=29511)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29511" in cmd
+    assert cmd[-len(argv):] == argv and cmd[-len(argv) - 1].endswith("bench.py")
+    assert B.launch_plan(8, {"WORLD_SIZE": "8"}, argv) is None
+    assert B.launch_plan(None, {"WORLD_SIZE": "4"}, []) is None
+    assert B.launch_plan(1, {}, ["--gpus", "1"]) is None
+    assert B.launch_plan(None, {}, []) is None
+    with pytest.raises(SystemExit) as e:
+        B.launch_plan(8, {"WORLD_SIZE": "1"}, argv)
+    assert e.value.code == 2
+    with pytest.raises(SystemExit) as e:
+        B.launch_plan(2, {"WORLD_SIZE": "4"}, argv)
+    assert e.value.code == 2
+
+
+def _run_bench(args, extra_env=None):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                           "MASTER_ADDR", "MASTER_PORT")}
+    env.update(extra_env or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True,
+                       text=True, env=env, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_spawns_n_ranks_itself():
+    """The real launch path, no wrapper: `bench.py --gpus 2` starts two ranks that join one
+    gloo group (--launch-probe stops before any GPU call); rank 0's line says so."""
+    rc, out, err = _run_bench(["--gpus", "2", "--launch-probe"])
+    assert rc == 0, err[-2000:]
+    assert out == {"n_gpus": 2, "dist_backend": "gloo", "dist_world": 2, "rank": 0}
+    rc, out, err = _run_bench(["--gpus", "1", "--launch-probe"])
+    assert rc == 0 and out["n_gpus"] == 1 and out["dist_world"] == 1
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    rc, out, err = _run_bench(["--gpus", "4", "--launch-probe"], {"WORLD_SIZE": "2"})
+    assert rc == 2 and out is None and "WORLD_SIZE=2" in err
