@@ -3,6 +3,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <string>
+
 #include "fm_common.h"
 
 namespace fm {
@@ -33,6 +35,18 @@ extern "C" int fm_abi_sizes(int32_t* gram_args, int32_t* solve_args) {
     *gram_args = (int32_t)sizeof(fm_gram_args);
     *solve_args = (int32_t)sizeof(fm_solve_args);
     return FM_OK;
+}
+
+extern "C" int64_t fm_struct_size(const char* name) {
+    if (name == nullptr) return -1;
+    const std::string n(name);
+    if (n == "fm_gram_args") return (int64_t)sizeof(fm_gram_args);
+    if (n == "fm_solve_args") return (int64_t)sizeof(fm_solve_args);
+    if (n == "fm_select_args") return (int64_t)sizeof(fm_select_args);
+    if (n == "fm_universe_args") return (int64_t)sizeof(fm_universe_args);
+    if (n == "fm_ts_args") return (int64_t)sizeof(fm_ts_args);
+    if (n == "fm_chars_args") return (int64_t)sizeof(fm_chars_args);
+    return -1;
 }
 
 extern "C" int fm_device_arch(char* buf, int32_t len) {

@@ -160,6 +160,34 @@ __global__ __launch_bounds__(ET) void probe_kernel(const double* __restrict__ sr
     if (threadIdx.x == 0) atomicAdd(out, s);
 }
 
+// The FP64 panel as two 32-bit planes (high words, low words): the selects order values by
+// their high words alone (half the bytes), and the Gram re-reads the high plane right after
+// them, from the memory-side cache.  16-byte loads (two rows), 8-byte stores per plane.
+__global__ __launch_bounds__(ET) void split_planes_kernel(const double* __restrict__ cols, int64_t stride,
+                                                          int ncols, int64_t nrows, uint32_t* __restrict__ hi,
+                                                          uint32_t* __restrict__ lo, int64_t pstride) {
+    const int64_t npair = (nrows + 1) / 2;
+    const int64_t total = npair * ncols;
+    for (int64_t i = (int64_t)blockIdx.x * ET + threadIdx.x; i < total; i += (int64_t)gridDim.x * ET) {
+        const int64_t c = i / npair, p = i - c * npair, r = 2 * p;
+        const double* src = cols + c * stride + r;
+        uint32_t* h = hi + c * pstride + r;
+        uint32_t* l = lo + c * pstride + r;
+        if (r + 1 < nrows && (((uintptr_t)src | (uintptr_t)h | (uintptr_t)l) & 7) == 0 && (((uintptr_t)src) & 15) == 0) {
+            const double2 v = *(const double2*)src;
+            const uint64_t a = (uint64_t)__double_as_longlong(v.x), b = (uint64_t)__double_as_longlong(v.y);
+            *(uint2*)h = make_uint2((uint32_t)(a >> 32), (uint32_t)(b >> 32));
+            *(uint2*)l = make_uint2((uint32_t)a, (uint32_t)b);
+        } else {
+            for (int64_t k = r; k < r + 2 && k < nrows; ++k) {
+                const uint64_t a = (uint64_t)__double_as_longlong(cols[c * stride + k]);
+                hi[c * pstride + k] = (uint32_t)(a >> 32);
+                lo[c * pstride + k] = (uint32_t)a;
+            }
+        }
+    }
+}
+
 int zsplit(int64_t max_len) {
     // split long segments so every launch has >= ~2k workgroups in flight on 256 CUs
     int64_t z = (max_len + 4 * ET - 1) / (4 * ET);
@@ -243,6 +271,19 @@ extern "C" int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int3
                        month0, nmonths, nfirms, rate_thr(nan_rate), rate_thr(0.25 * nan_rate),
                        rate_thr(nyse_rate), rate_thr(0.3), cols, col_stride, me, nyse);
     FM_CHECK_LAUNCH("fm_gen_panel");
+    return FM_OK;
+}
+
+extern "C" int fm_split_planes(const double* cols, int64_t col_stride, int32_t ncols, int64_t nrows,
+                               uint32_t* hi, uint32_t* lo, int64_t plane_stride, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(cols && hi && lo, "fm_split_planes: null pointer");
+    FM_REQUIRE(ncols >= 0 && nrows >= 0 && col_stride >= nrows && plane_stride >= nrows,
+               "fm_split_planes: bad sizes");
+    if (ncols == 0 || nrows == 0) return FM_OK;
+    hipLaunchKernelGGL(split_planes_kernel, dim3(4096), dim3(ET), 0, (hipStream_t)stream, cols, col_stride, ncols,
+                       nrows, hi, lo, plane_stride);
+    FM_CHECK_LAUNCH("fm_split_planes");
     return FM_OK;
 }
 

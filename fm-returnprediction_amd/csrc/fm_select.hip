@@ -20,6 +20,7 @@
 #include "fm_common.h"
 
 #include "fm_select_dev.h"
+#include "fm_npsel_dev.h"
 
 #ifndef FM_SELECT_STREAM_VPT
 #define FM_SELECT_STREAM_VPT 24   // values per thread above which fm_select streams the units
@@ -37,31 +38,10 @@
 namespace fm {
 namespace {
 
-template <int VPT, bool FB>
+template <int VPT>
 __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
     __shared__ SelSmem sm;
-    if (!FB) {
-        select_unit_wg<VPT>(a, blockIdx.x, blockIdx.y, sm);
-        return;
-    }
-    // Each workgroup scans a contiguous range of units with one coalesced load of the marks
-    // per 256 units (a unit-by-unit scan would pay one memory round trip per unit), then
-    // redoes the marked ones, lowest unit first (each thread clears its own mark).
-    const int64_t nunits = (int64_t)a.nseg * a.ncols;
-    const int64_t per = (nunits + gridDim.x - 1) / gridDim.x;
-    const int64_t u0 = (int64_t)blockIdx.x * per, u1 = u0 + per < nunits ? u0 + per : nunits;
-    for (int64_t b = u0; b < u1; b += ST) {
-        const int64_t u = b + threadIdx.x;
-        bool mark = u < u1 && a.nvalid[u] == -1;
-        while (true) {
-            const uint64_t pick = block_min_u64<SNW>(mark ? (uint64_t)u : SENT, sm.u64s);
-            if (pick == SENT) break;   // block-uniform
-            if ((uint64_t)u == pick) mark = false;
-            __syncthreads();
-            select_unit_wg<VPT>(a, (int)(pick % a.nseg), (int)(pick / a.nseg), sm);
-            __syncthreads();
-        }
-    }
+    select_unit_wg<VPT>(a, blockIdx.x, blockIdx.y, sm);
 }
 
 // Segments past the register budget (> 20,480 rows: a daily-frequency panel, a huge
@@ -161,34 +141,143 @@ __device__ __forceinline__ void stream_unit(const SelArgs& a, int s, int c, SelS
         a.lo[o] = lo;
         a.hi[o] = hi;
         if (a.nvalid) a.nvalid[o] = n;
+        if (zero_cut(a, lo, hi)) sel_push(a, o);
     }
 }
 
-// FB == false: one unit per workgroup (grid nseg x ncols).  FB == true: a fixed grid that
-// walks every unit and redoes those the long-segment kernel marked with nvalid == -1 (its
-// tail path could not finish them), lowest unit first, as select_kernel's fallback does.
-template <bool FB>
-__global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
-    __shared__ SelSmem sm;
-    if (!FB) {
-        stream_unit(a, blockIdx.x, blockIdx.y, sm);
-        return;
+
+// ---- The fix-up pass: one launch after every fm_select path.  The fast kernels put on
+// fm_select_args.ws's worklist the units they could not finish (marked nvalid = -1: ranks
+// past their tail windows, candidate overflow, ambiguous high keys) and the units whose numpy
+// cut came out exactly +-0; each workgroup here redoes its share of the list exactly (the
+// register workgroup path up to VPT values per thread, else streaming) and, for a zero cut
+// of a unit whose values hold both -0.0 and +0.0, replays numpy's partition to get the
+// reference's sign (fm_npsel_dev.h).  An empty list costs one load per workgroup; the last
+// workgroup to finish leaves the list empty for the next call.
+constexpr int ZS_LDS = 6144;               // units of up to this many rows replay in LDS
+constexpr int FIX_GRID = 256;
+constexpr int64_t ZS_GLOBAL_BYTES = 64ll << 20;   // longer units: one global slot per workgroup
+
+union FixSmem {
+    SelSmem sel;
+    double arr[ZS_LDS];
+};
+
+// wave 0: the exactly-zero numpy cuts of unit (s, c), written by this workgroup just before
+template <class A>
+__device__ void zero_sign_unit(const SelArgs& a, int s, int c, A arr) {
+    const int lane = lane_id();
+    const int64_t o = (int64_t)c * a.nseg + s;
+    auto ld = [](const double* p) {
+        return __longlong_as_double(
+            (long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
+    const double lo = ld(a.lo + o), hi = ld(a.hi + o);
+    const bool zl = lo == 0.0, zh = hi == 0.0;
+    if (!zl && !zh) return;
+    const int64_t r0 = a.seg_off[s];
+    const int L = (int)(a.seg_off[s + 1] - r0);
+    const double* src = a.cols + (int64_t)c * a.col_stride + r0;
+    const uint8_t* msk = a.mask ? a.mask + r0 : nullptr;
+    // the values np.percentile sees: the unit's non-NaN (row-mask selected) rows, frame order
+    auto fill = [&](bool& both) -> int {
+        int cnt = 0;
+        bool ng = false, ps = false;
+        for (int b = 0; b < L; b += WAVE) {
+            const int r = b + lane;
+            double x = r < L ? src[r] : (double)NAN;
+            if (msk != nullptr && r < L && msk[r] == 0) x = NAN;
+            const bool v = !isnan(x);
+            const uint64_t bal = __ballot(v);
+            if (v) arr.st(cnt + mask_rank(bal), x);
+            cnt += (int)__popcll(bal);
+            const bool z = x == 0.0;
+            ng = ng || (z && __double_as_longlong(x) < 0);
+            ps = ps || (z && __double_as_longlong(x) >= 0);
+        }
+        arr.sync();
+        both = __ballot(ng) != 0ull && __ballot(ps) != 0ull;
+        return cnt;
+    };
+    bool both = false;
+    int n = fill(both);
+    if (!both) return;   // one kind of zero: the key order already gave numpy's bits
+    for (int t = 0; t < 2; ++t) {
+        if (t == 0 ? !zl : !zh) continue;
+        if (t == 1 && zl) n = fill(both);   // each np.percentile call partitions its own copy
+        const double q = t == 0 ? a.q_lo : a.q_hi;
+        int i, j;
+        double g;
+        qranks(n, q, 0, i, j, g);
+        const bool top = (double)(n - 1) * q >= (double)(n - 1);
+        double va, vb;
+        np_percentile_pair(arr, n, top ? -1 : i, va, vb);
+        const double r = qlerp(va, vb, g, 0);
+        if (lane == 0) (t == 0 ? a.lo : a.hi)[o] = r;
     }
-    const int64_t nunits = (int64_t)a.nseg * a.ncols;
-    const int64_t per = (nunits + gridDim.x - 1) / gridDim.x;
-    const int64_t u0 = (int64_t)blockIdx.x * per, u1 = u0 + per < nunits ? u0 + per : nunits;
-    for (int64_t b = u0; b < u1; b += ST) {
-        const int64_t u = b + threadIdx.x;
-        bool mark = u < u1 && a.nvalid[u] == -1;
-        while (true) {
-            const uint64_t pick = block_min_u64<SNW>(mark ? (uint64_t)u : SENT, sm.u64s);
-            if (pick == SENT) break;   // block-uniform
-            if ((uint64_t)u == pick) mark = false;
-            __syncthreads();
-            stream_unit(a, (int)(pick % a.nseg), (int)(pick / a.nseg), sm);
-            __syncthreads();
+}
+
+template <int VPT>   // VPT == 0: the streaming exact path
+__global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs, int zs_len) {
+    __shared__ FixSmem sm;
+    SelCtl* ctl = a.ctl;
+    SelArgs b = a;
+    b.ctl = nullptr;
+    const uint32_t nw = __hip_atomic_load(&ctl->nwork, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = blockIdx.x; i < nw; i += gridDim.x) {
+        const uint32_t u = ctl->work[i];
+        const int s = (int)(u % (uint32_t)b.nseg), c = (int)(u / (uint32_t)b.nseg);
+        if constexpr (VPT > 0) select_unit_wg<VPT>(b, s, c, sm.sel);
+        else stream_unit(b, s, c, sm.sel);
+        __threadfence();
+        __syncthreads();
+        if (b.lerp_mode == 0 && threadIdx.x < WAVE) {
+            const int64_t L = b.seg_off[s + 1] - b.seg_off[s];
+            if (L <= ZS_LDS) zero_sign_unit(b, s, c, NpLds{sm.arr});
+            else zero_sign_unit(b, s, c, NpGlobal{zs + (int64_t)blockIdx.x * zs_len});
+        }
+        __threadfence();
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t t = atomicAdd(&ctl->done, 1u);
+        if (t == gridDim.x - 1) {
+            __hip_atomic_store(&ctl->nwork, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+int64_t ws_list_bytes(int64_t nunits) { return ((int64_t)offsetof(SelCtl, work) + 4 * nunits + 255) / 256 * 256; }
+int fix_grid(int max_seg_len) {
+    if (max_seg_len <= ZS_LDS) return FIX_GRID;
+    const int64_t g = ZS_GLOBAL_BYTES / ((int64_t)max_seg_len * 8);
+    return (int)(g < 1 ? 1 : (g < FIX_GRID ? g : FIX_GRID));
+}
+int64_t ws_bytes(int32_t nseg, int32_t ncols, int32_t max_seg_len) {
+    const int64_t list = ws_list_bytes((int64_t)nseg * ncols);
+    return max_seg_len <= ZS_LDS ? list : list + (int64_t)fix_grid(max_seg_len) * max_seg_len * 8;
+}
+
+void launch_fixup(const SelArgs& a, int max_seg_len, hipStream_t st) {
+    const int vpt = (max_seg_len + ST - 1) / ST;
+    const int g = fix_grid(max_seg_len);
+    double* zs = (double*)((char*)a.ctl + ws_list_bytes((int64_t)a.nseg * a.ncols));
+    const int zl = max_seg_len;
+    if (vpt <= 2) hipLaunchKernelGGL(select_fixup_kernel<2>, dim3(g), dim3(ST), 0, st, a, zs, zl);
+    else if (vpt <= 4) hipLaunchKernelGGL(select_fixup_kernel<4>, dim3(g), dim3(ST), 0, st, a, zs, zl);
+    else if (vpt <= 8) hipLaunchKernelGGL(select_fixup_kernel<8>, dim3(g), dim3(ST), 0, st, a, zs, zl);
+    else if (vpt <= 16) hipLaunchKernelGGL(select_fixup_kernel<16>, dim3(g), dim3(ST), 0, st, a, zs, zl);
+    else if (vpt <= 20) hipLaunchKernelGGL(select_fixup_kernel<20>, dim3(g), dim3(ST), 0, st, a, zs, zl);
+    else if (vpt <= FM_SELECT_STREAM_VPT) hipLaunchKernelGGL(select_fixup_kernel<FM_SELECT_STREAM_VPT>, dim3(g), dim3(ST), 0, st, a, zs, zl);
+    else hipLaunchKernelGGL(select_fixup_kernel<0>, dim3(g), dim3(ST), 0, st, a, zs, zl);
+}
+
+// One unit per workgroup (grid nseg x ncols).
+__global__ __launch_bounds__(ST) void select_stream_kernel(SelArgs a) {
+    __shared__ SelSmem sm;
+    stream_unit(a, blockIdx.x, blockIdx.y, sm);
 }
 
 // Long segments (6,145 .. 20,480 rows: C5's 20,000-firm months, a daily panel's short
@@ -535,8 +624,8 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
             }
         }
     }
-    if (!ok) {   // redone by select_stream_kernel<true>
-        if (tid == 0) a.nvalid[o] = -1;
+    if (!ok) {   // redone by the fix-up kernel
+        if (tid == 0) sel_mark(a, o);
         return;
     }
     if (a.center != nullptr) {
@@ -554,6 +643,7 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
         a.lo[o] = lo;
         a.hi[o] = hi;
         a.nvalid[o] = n;
+        if (zero_cut(a, lo, hi)) sel_push(a, o);
     }
 }
 
@@ -616,6 +706,19 @@ __device__ __forceinline__ void hk_load(const double* col, int L, uint32_t (&hk)
         const int nrec = rem > 0 ? (rem < LT ? rem : LT) * 8 : 0;
         const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(col + (rem > 0 ? v * LT : 0)), 0, nrec,
                                                           0x00020000);
+        hk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb, 0, 0);
+    }
+}
+
+// ... or from the high-word plane (4 bytes per value read instead of 8)
+template <int VPT>
+__device__ __forceinline__ void hk_load_plane(const uint32_t* hp, int L, uint32_t (&hk)[VPT]) {
+    const uint32_t lb = (uint32_t)threadIdx.x * 4u;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const int rem = L - v * LT;
+        const int nrec = rem > 0 ? (rem < LT ? rem : LT) * 4 : 0;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(hp + (rem > 0 ? v * LT : 0)), 0, nrec, 0x00020000);
         hk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb, 0, 0);
     }
 }
@@ -786,8 +889,8 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
         lo = qlerp(kval(sm.res[0]), kval(sm.res[1]), g0, a.lerp_mode);
         hi = qlerp(kval(sm.res[2]), kval(sm.res[3]), g1, a.lerp_mode);
     }
-    if (!ok) {   // redone by select_stream_kernel<true>
-        if (tid == 0) a.nvalid[o] = -1;
+    if (!ok) {   // redone by the fix-up kernel
+        if (tid == 0) sel_mark(a, o);
     } else {
         if (a.center != nullptr) {
             // Gram pivot: the midpoint of the cuts, else of the finite range (no +-inf here:
@@ -814,6 +917,7 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
             a.lo[o] = lo;
             a.hi[o] = hi;
             a.nvalid[o] = n;
+            if (zero_cut(a, lo, hi)) sel_push(a, o);
         }
     }
     __syncthreads();   // the LDS is rewritten by the next unit
@@ -832,7 +936,10 @@ __global__ __launch_bounds__(LT, 6) void select_long_hk_kernel(SelArgs a) {
         return;
     }
     uint32_t hk[VPT];
-    hk_load<VPT>(a.cols + (int64_t)c * a.col_stride + a.seg_off[s], (int)(a.seg_off[s + 1] - a.seg_off[s]), hk);
+    if (a.hp != nullptr)
+        hk_load_plane<VPT>(a.hp + (int64_t)c * a.pstride + a.seg_off[s], (int)(a.seg_off[s + 1] - a.seg_off[s]), hk);
+    else
+        hk_load<VPT>(a.cols + (int64_t)c * a.col_stride + a.seg_off[s], (int)(a.seg_off[s + 1] - a.seg_off[s]), hk);
     hk_unit<VPT>(a, s, c, hk, sm);
 }
 
@@ -870,11 +977,8 @@ int launch_select_long(const SelArgs& a, int max_seg_len, hipStream_t st) {
 }
 
 template <int VPT>
-void launch_select(const SelArgs& a, int ncols, hipStream_t st, bool fallback) {
-    if (fallback)
-        hipLaunchKernelGGL((select_kernel<VPT, true>), dim3(256), dim3(ST), 0, st, a);
-    else
-        hipLaunchKernelGGL((select_kernel<VPT, false>), dim3(a.nseg, ncols), dim3(ST), 0, st, a);
+void launch_select(const SelArgs& a, int ncols, hipStream_t st) {
+    hipLaunchKernelGGL((select_kernel<VPT>), dim3(a.nseg, ncols), dim3(ST), 0, st, a);
 }
 
 __device__ __forceinline__ int64_t unit_of(const SelArgs& a, int64_t k) {
@@ -927,7 +1031,7 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
         const int n = r.n;
         const bool ok = r.ok;
         if (!ok) {
-            if (lane == 0 && a.nvalid) a.nvalid[u] = -1;   // redone by the fallback pass
+            if (lane == 0) sel_mark(a, u);   // redone by the fix-up kernel
         } else {
             if (a.center != nullptr && lane == 0) a.center[u] = r.cen;
             if (!early) {
@@ -976,6 +1080,7 @@ __global__ __launch_bounds__(ST, 2) void select_wave_kernel(SelArgs a) {
                 a.lo[u] = lo;
                 a.hi[u] = hi;
                 if (a.nvalid) a.nvalid[u] = n;
+                if (zero_cut(a, lo, hi)) sel_push(a, u);
             }
         }
         if (!more) break;
@@ -1206,8 +1311,8 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
             hi = sm.res[1];
         }
         if (apply && !ok) {
-            // redone by the workgroup kernel's fallback pass
-            if (threadIdx.x == 0) a.nvalid[u] = -1;
+            // redone by the fix-up kernel
+            if (threadIdx.x == 0) sel_mark(a, u);
         } else if (h == 0) {
             double cen = 0.5 * (lo + hi);
             if (!isfinite(cen)) {
@@ -1220,6 +1325,7 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
                 a.lo[u] = lo;
                 a.hi[u] = hi;
                 if (a.nvalid) a.nvalid[u] = n;
+                if (zero_cut(a, lo, hi)) sel_push(a, u);
             }
         } else if (!isfinite(0.5 * (lo + hi))) {
             // wave 1's half of the finite range for the pivot fallback
@@ -1232,6 +1338,314 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
         if ((ok || !apply) && a.center && !isfinite(0.5 * (lo + hi)) && threadIdx.x == 0) {
             // pivot fallback: the midpoint of the finite range (both halves), else 0
             const double m1 = hw_min(sm.res[0], sm.tv[0]), m2 = hw_max(sm.res[1], sm.tv[1]);
+            double cen = 0.5 * (m1 + m2);
+            a.center[u] = isfinite(cen) ? cen : 0.0;
+        }
+        __syncthreads();   // LDS state is rewritten by the next unit
+        if (!more) break;
+        k = kn;
+        s_cur = s_nx;
+        c_cur = c_nx;
+        L = Ln;
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Two-wave units on the HIGH-WORD plane (fm_select_args.hi_plane: the panel's high 32 bits,
+// fm_split_planes): select_pair_kernel's structure with every step before the final pick on
+// 32-bit order keys (hkey), so a unit reads half the bytes and holds half the registers:
+//   1. per wave: valid count, lane min / max keys (a lane holding +-inf or a NaN whose payload
+//      is all in the low word -- keys 0 / HK_MAX -- sends the unit to the fix-up kernel);
+//   2. wave 0 / 1: T = the kr-th smallest of the 128 lane-extreme keys of its tail, so at
+//      least kr + 1 values have keys <= T: the values with key <= T are a prefix of the sorted
+//      order holding both target ranks;
+//   3. per wave: (key, row) of those values compacted to LDS, both tails; the next unit's
+//      loads are issued here;
+//   4. wave t sorts tail t's candidates by (key, row) and gathers the FP64 values at the two
+//      target ranks from the column (4 scattered loads per unit); when high words tie at those
+//      ranks every tied candidate is gathered and the tie broken by the full keys.
+#ifndef FM_PAIR_HK_WGS
+#define FM_PAIR_HK_WGS 12   // resident two-wave workgroups per CU (register budget and grid)
+#endif
+struct PairHkSmem {
+    uint32_t sk[2][2][WAVE];     // [wave][lo / hi][lane] sorted lane-extreme keys
+    uint64_t cand[2][2][WCAP];   // [wave][lo / hi] (key << 32 | row) candidates
+    int ni[2][4];
+    uint32_t tv[2];
+    double res[2];
+    double fr[2];   // wave 1's half of the finite range (pivot fallback)
+    int okv[2];
+};
+
+// Values at ranks ra <= rb (rb <= ra + 1) of one tail's candidates L1 ++ L2 (c <= 64 R);
+// tail 1 holds complemented keys (ranks from the top).  false: cannot decide (never expected).
+template <int R>
+__device__ __forceinline__ bool pick_hk(uint64_t* L1, int c1, const uint64_t* L2, int c2, int ra, int rb, int tail,
+                                        const double* col, double& va, double& vb) {
+    const int lane = lane_id();
+    const int c = c1 + c2;
+    uint64_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane + WAVE * r;
+        v[r] = e < c1 ? L1[e] : (e < c ? L2[e - c1] : SENT);
+    }
+    wave_sort<R>(v);
+    auto at = [&](int e) -> uint64_t {
+        const int q = e >> 6, l = e & 63;
+        uint64_t x = readlane_u64(v[0], l);
+        static_for<1, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            const uint64_t t = readlane_u64(v[r], l);
+            x = q == r ? t : x;
+        });
+        return x;
+    };
+    const uint64_t ea = at(ra), eb = at(rb);
+    const uint32_t Ka = (uint32_t)(ea >> 32), Kb = (uint32_t)(eb >> 32);
+    int p0 = 0, m = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t k = (uint32_t)(v[r] >> 32);
+        const bool real = v[r] != SENT;
+        p0 += (int)__popcll(__ballot(real && k < Ka));
+        m += (int)__popcll(__ballot(real && k >= Ka && k <= Kb));
+    }
+    if (m == rb - ra + 1 && (ra == rb || Ka != Kb)) {   // distinct high words: two gathers
+        va = col[(uint32_t)ea];
+        vb = col[(uint32_t)eb];
+        return true;
+    }
+    // high words tie at the target ranks: full keys of the tied candidates [p0, p0 + m),
+    // sorted in this wave's own (already loaded) list space
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane + WAVE * r;
+        if (e >= p0 && e < p0 + m) {
+            const double x = col[(uint32_t)v[r]];
+            L1[e - p0] = tail == 0 ? dkey(x) : ~dkey(x);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint64_t w[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane + WAVE * r;
+        w[r] = e < m ? L1[e] : SENT;
+    }
+    wave_sort<R>(w);
+    auto atw = [&](int e) -> uint64_t {
+        const int q = e >> 6, l = e & 63;
+        uint64_t x = readlane_u64(w[0], l);
+        static_for<1, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            const uint64_t t = readlane_u64(w[r], l);
+            x = q == r ? t : x;
+        });
+        return x;
+    };
+    const uint64_t fa = atw(ra - p0), fb = atw(rb - p0);
+    va = kval(tail == 0 ? fa : ~fa);
+    vb = kval(tail == 0 ? fb : ~fb);
+    return true;
+}
+
+template <int VPH>
+__global__ __launch_bounds__(2 * WAVE, FM_PAIR_HK_WGS / 2) void select_pair_hk_kernel(SelArgs a) {
+    __shared__ PairHkSmem sm;
+    const int lane = lane_id();
+    const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
+    int64_t k = blockIdx.x;
+    if (k >= nunits) return;   // block-uniform
+    const int ncols = a.ncols;
+    const int G = (int)gridDim.x;
+    const int dS = G / ncols, dC = G - (G / ncols) * ncols;
+    int s_cur = (int)blockIdx.x / ncols;
+    int c_cur = (int)blockIdx.x - s_cur * ncols;
+    uint32_t xk[VPH];
+    // the unit's raw high words: one buffer descriptor per unit (its range check reads 0 past
+    // the month end; masked after), the lane's byte offset the only VGPR
+    auto load = [&](int s, int c) -> int {
+        const int64_t r0 = a.seg_off[s];
+        const int L = (int)(a.seg_off[s + 1] - r0);
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.hp + (int64_t)c * a.pstride + r0), 0,
+                                                          L > 0 ? L * 4 : 0, 0x00020000);
+        uint32_t lb = (uint32_t)(h * WAVE + lane) * 4u;
+        asm volatile("" : "+v"(lb));
+#pragma unroll
+        for (int v = 0; v < VPH; ++v)
+            xk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb + (uint32_t)(v * 2 * WAVE * 4), 0, 0);
+        return L;
+    };
+    auto finite_range = [&](int s, int c, double& m1, double& m2) {
+        const double* base = a.cols + (int64_t)c * a.col_stride + a.seg_off[s];
+        const int Lu = (int)(a.seg_off[s + 1] - a.seg_off[s]);
+        m1 = NAN;
+        m2 = NAN;
+        for (int r = h * WAVE + lane; r < Lu; r += 2 * WAVE) {
+            const double x = base[r];
+            m1 = hw_min(m1, isfinite(x) ? x : NAN);
+            m2 = hw_max(m2, isfinite(x) ? x : NAN);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            m1 = hw_min(m1, xor_lanes_f64(m1, o));
+            m2 = hw_max(m2, xor_lanes_f64(m2, o));
+        }
+    };
+    int L = load(s_cur, c_cur);
+    while (true) {
+        const int64_t u = (int64_t)c_cur * a.nseg + s_cur;
+        const int64_t kn = k + gridDim.x;
+        const bool more = kn < nunits;
+        int s_nx = s_cur + dS, c_nx = c_cur + dC;
+        if (c_nx >= ncols) {
+            c_nx -= ncols;
+            ++s_nx;
+        }
+        int Ln = 0;
+        const int row0 = h * WAVE + lane;
+        // ---- 1. keys (rows past the month end -> HK_NONE), count, lane min / max keys
+        const int lim = L - row0;
+        int nh = 0;
+        uint32_t kmn = HK_NONE, kmx2 = 0;
+#pragma unroll
+        for (int v = 0; v < VPH; ++v) {
+            const uint32_t kk = v * 2 * WAVE < lim ? hkey(xk[v]) : HK_NONE;
+            xk[v] = kk;
+            nh += (int)__popcll(__ballot(kk <= HK_MAX));
+            kmn = min(kmn, kk);
+            kmx2 = max(kmx2, kk + 0x1FFFFEu);   // NaN / absent keys wrap below every valid one
+            asm volatile("" : "+s"(nh), "+v"(kmn), "+v"(kmx2));
+        }
+        const bool tvalid = kmn <= HK_MAX;
+        const uint32_t kmx = kmx2 - 0x1FFFFEu;
+        const bool amb = tvalid && (kmn == 0u || kmx == HK_MAX);
+        {
+            uint32_t ta[1] = {tvalid ? kmn : HK_NONE}, tb[1] = {tvalid ? HK_MAX - kmx : HK_NONE};
+            wave_sort32<1>(ta);
+            wave_sort32<1>(tb);
+            sm.sk[h][0][lane] = ta[0];
+            sm.sk[h][1][lane] = tb[0];
+        }
+        const int ambw = (int)__popcll(__ballot(amb));
+        if (lane == 0) {
+            sm.ni[h][0] = nh;
+            sm.ni[h][3] = ambw;
+        }
+        __syncthreads();
+        const int n = sm.ni[0][0] + sm.ni[1][0];
+        const int mode = a.lerp_mode;
+        const bool apply = n >= a.min_count && n > 0;
+        int i0 = 0, j0 = 0, i1 = 0, j1 = 0;
+        double g0 = 0.0, g1 = 0.0;
+        if (apply) {
+            qranks(n, a.q_lo, mode, i0, j0, g0);
+            qranks(n, a.q_hi, mode, i1, j1, g1);
+        }
+        bool ok = apply && sm.ni[0][3] + sm.ni[1][3] == 0;
+        if (ok) {
+            // ---- 2. this wave's tail threshold: the kr-th of the 128 lane-extreme keys
+            const int t = h;
+            const int kr = t == 0 ? j0 : n - 1 - i1;
+            uint32_t T = HK_NONE;
+            if (kr < 2 * WAVE) {
+                const uint32_t mine = sm.sk[0][t][lane], other = sm.sk[1][t][lane];
+                const int q0 = lane + count_below_u32(sm.sk[1][t], mine, false);
+                const int q1 = lane + count_below_u32(sm.sk[0][t], other, true);
+                const uint64_t m0 = __ballot(q0 == kr), m1 = __ballot(q1 == kr);
+                if (m0) T = (uint32_t)__builtin_amdgcn_readlane((int)mine, __builtin_ctzll(m0));
+                else if (m1) T = (uint32_t)__builtin_amdgcn_readlane((int)other, __builtin_ctzll(m1));
+            }
+            if (lane == 0) {
+                sm.tv[h] = T;
+                sm.okv[h] = T <= HK_MAX ? 1 : 0;
+            }
+            __syncthreads();
+            ok = sm.okv[0] != 0 && sm.okv[1] != 0;   // block-uniform
+        }
+        double lo = NAN, hi = NAN;
+        bool prefetched = false;
+        if (ok) {
+            // ---- 3. (key, row) candidates of both tails from this wave's half
+            const uint32_t tlo = sm.tv[0], thi = sm.tv[1];
+            int clo = 0, chi = 0;
+            uint64_t* Ll = sm.cand[h][0];
+            uint64_t* Lh = sm.cand[h][1];
+#pragma unroll
+            for (int v = 0; v < VPH; ++v) {
+                const uint32_t kk = xk[v];
+                const bool bl = kk <= tlo, bh = HK_MAX - kk <= thi;   // NaN / absent keys wrap above thi
+                const uint64_t ml = __ballot(bl), mh = __ballot(bh);
+                const uint64_t row = (uint64_t)(uint32_t)(row0 + v * 2 * WAVE);
+                if (ml) {
+                    if (bl) Ll[(clo + mask_rank(ml)) & (WCAP - 1)] = ((uint64_t)kk << 32) | row;
+                    clo += (int)__popcll(ml);
+                }
+                if (mh) {
+                    if (bh) Lh[(chi + mask_rank(mh)) & (WCAP - 1)] = ((uint64_t)(HK_MAX - kk) << 32) | row;
+                    chi += (int)__popcll(mh);
+                }
+            }
+            if (lane == 0) {
+                sm.ni[h][1] = clo;
+                sm.ni[h][2] = chi;
+            }
+            // xk is dead from here on: the next unit's loads fly during the sorts and gathers
+            if (more) Ln = load(s_nx, c_nx);
+            prefetched = true;
+            __syncthreads();
+            // ---- 4. one tail per wave over both halves' candidates
+            const int t = h;
+            const int c0 = sm.ni[0][1 + t], c1 = sm.ni[1][1 + t];
+            const int cc = c0 + c1;
+            bool good = c0 <= WCAP && c1 <= WCAP && cc <= 4 * WAVE;
+            if (good) {
+                const double* col = a.cols + (int64_t)c_cur * a.col_stride + a.seg_off[s_cur];
+                const int ra = t == 0 ? i0 : n - 1 - j1, rb = t == 0 ? j0 : n - 1 - i1;
+                double va = NAN, vb = NAN;
+                if (cc <= 2 * WAVE) good = pick_hk<2>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, t, col, va, vb);
+                else good = pick_hk<4>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, t, col, va, vb);
+                // tail 1: ra / rb count from the top: va is the value at rank j1, vb at i1
+                if (lane == 0) sm.res[h] = t == 0 ? qlerp(va, vb, g0, mode) : qlerp(vb, va, g1, mode);
+            }
+            if (lane == 0) sm.okv[h] = good ? 1 : 0;
+            __syncthreads();
+            ok = sm.okv[0] != 0 && sm.okv[1] != 0;   // block-uniform
+            lo = sm.res[0];
+            hi = sm.res[1];
+        }
+        if (apply && !ok) {
+            if (threadIdx.x == 0) sel_mark(a, u);   // redone by the fix-up kernel
+        } else if (h == 0) {
+            double cen = 0.5 * (lo + hi);
+            if (!isfinite(cen)) {
+                double m1, m2;
+                finite_range(s_cur, c_cur, m1, m2);
+                if (lane == 0) sm.res[0] = m1, sm.res[1] = m2;
+            }
+            if (lane == 0) {
+                if (a.center && isfinite(cen)) a.center[u] = cen;
+                a.lo[u] = lo;
+                a.hi[u] = hi;
+                if (a.nvalid) a.nvalid[u] = n;
+                if (zero_cut(a, lo, hi)) sel_push(a, u);
+            }
+        } else if (!isfinite(0.5 * (lo + hi))) {
+            double m1, m2;
+            finite_range(s_cur, c_cur, m1, m2);
+            if (lane == 0) sm.fr[0] = m1, sm.fr[1] = m2;
+        }
+        if (more && !prefetched) Ln = load(s_nx, c_nx);
+        __syncthreads();
+        if ((ok || !apply) && a.center && !isfinite(0.5 * (lo + hi)) && threadIdx.x == 0) {
+            const double m1 = hw_min(sm.res[0], sm.fr[0]), m2 = hw_max(sm.res[1], sm.fr[1]);
             double cen = 0.5 * (m1 + m2);
             a.center[u] = isfinite(cen) ? cen : 0.0;
         }
@@ -1258,7 +1672,14 @@ int select_wave_grid(int64_t nunits) {
 }
 
 template <int VPH>
+void launch_select_pair_hk(const SelArgs& a, hipStream_t st);
+
+template <int VPH>
 void launch_select_pair(const SelArgs& a, hipStream_t st) {
+    if (a.hp != nullptr) {
+        launch_select_pair_hk<VPH>(a, st);
+        return;
+    }
     static int ncu = [] {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -1269,6 +1690,21 @@ void launch_select_pair(const SelArgs& a, hipStream_t st) {
     const int64_t nunits = (int64_t)a.nseg * a.ncols;
     const int64_t cap = (int64_t)ncu * 8;   // eight 2-wave workgroups per CU (4 waves / SIMD)
     hipLaunchKernelGGL((select_pair_kernel<VPH>), dim3((unsigned)(nunits < cap ? nunits : cap)), dim3(2 * WAVE),
+                       0, st, a);
+}
+
+template <int VPH>
+void launch_select_pair_hk(const SelArgs& a, hipStream_t st) {
+    static int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int64_t nunits = (int64_t)a.nseg * a.ncols;
+    const int64_t cap = (int64_t)ncu * FM_PAIR_HK_WGS;
+    hipLaunchKernelGGL((select_pair_hk_kernel<VPH>), dim3((unsigned)(nunits < cap ? nunits : cap)), dim3(2 * WAVE),
                        0, st, a);
 }
 
@@ -1390,11 +1826,31 @@ extern "C" int fm_select_cuts(const double* cols, int64_t col_stride, int32_t nc
                               const int64_t* seg_off, int32_t nseg, int32_t max_seg_len,
                               const uint8_t* row_mask, double q_lo, double q_hi,
                               int32_t min_count, int32_t lerp_mode, double* lo, double* hi,
-                              int32_t* nvalid, double* mean, double* sd, void* stream) {
-    const fm_select_args a{cols,    col_stride, ncols,    seg_off, nseg, max_seg_len, row_mask, q_lo,
-                           q_hi,    min_count,  lerp_mode, lo,     hi,   nvalid,      mean,     sd,
-                           nullptr};
+                              int32_t* nvalid, double* mean, double* sd, void* ws, void* stream) {
+    fm_select_args a{};
+    a.cols = cols;
+    a.col_stride = col_stride;
+    a.ncols = ncols;
+    a.seg_off = seg_off;
+    a.nseg = nseg;
+    a.max_seg_len = max_seg_len;
+    a.row_mask = row_mask;
+    a.q_lo = q_lo;
+    a.q_hi = q_hi;
+    a.min_count = min_count;
+    a.lerp_mode = lerp_mode;
+    a.lo = lo;
+    a.hi = hi;
+    a.nvalid = nvalid;
+    a.mean = mean;
+    a.sd = sd;
+    a.ws = ws;
     return fm_select(&a, stream);
+}
+
+extern "C" int64_t fm_select_ws_bytes(int32_t nseg, int32_t ncols, int32_t max_seg_len) {
+    if (nseg < 0 || ncols < 0 || max_seg_len < 0) return -1;
+    return fm::ws_bytes(nseg, ncols, max_seg_len);
 }
 
 namespace fm {
@@ -1453,6 +1909,7 @@ int universe_separately(const fm_select_args& x, const fm_universe_args* u, void
     y.lo = u->cut_a;
     y.hi = u->cut_b;
     y.level = u->level;
+    y.ws = x.ws;
     return select_impl(&y, nullptr, stream);
 }
 
@@ -1471,9 +1928,15 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
                "fm_select_cuts: quantiles must be in [0,1]");
     if (nseg == 0) return FM_OK;
     FM_REQUIRE(x.level == nullptr || ncols == 1, "fm_select: level needs a single column");
+    FM_REQUIRE(x.ws != nullptr && x.nvalid != nullptr,
+               "fm_select: nvalid and ws (fm_select_ws_bytes, zeroed once) are required");
     SelArgs a{cols,        x.col_stride, seg_off, nseg,     ncols, row_mask, x.q_lo, x.q_hi,
               x.min_count, x.lerp_mode,  x.lo,    x.hi,     x.nvalid, x.mean, x.sd,  x.center,
               nullptr,     x.level};
+    a.ctl = (SelCtl*)x.ws;
+    a.hp = x.hi_plane;
+    a.pstride = x.plane_stride;
+    FM_REQUIRE(a.hp == nullptr || a.pstride > 0, "fm_select: hi_plane needs plane_stride > 0");
     hipStream_t st = (hipStream_t)stream;
     const int vpt = (max_seg_len + ST - 1) / ST;
     const bool long_path = vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && x.mean == nullptr &&
@@ -1496,8 +1959,8 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
         const int rc = launch_select_long(al, max_seg_len, st);
         if (rc != FM_OK) return rc;
         FM_CHECK_LAUNCH("fm_select_cuts(long)");
-        if (!FM_AB_NOFB) hipLaunchKernelGGL(select_stream_kernel<true>, dim3(256), dim3(ST), 0, st, a);
-        FM_CHECK_LAUNCH("fm_select_cuts(long fallback)");
+        if (!FM_AB_NOFB) launch_fixup(a, max_seg_len, st);
+        FM_CHECK_LAUNCH("fm_select_cuts(long fix-up)");
         // the level bytes by a streaming launch: writing them from the select kernel (a
         // re-read of the unmasked column, or unmasked registers + mask bits) measured no
         // faster, the register select being latency-bound at one workgroup per CU
@@ -1507,8 +1970,10 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
     if (vpt > FM_SELECT_STREAM_VPT) {
         // longer still, or row masks / moments: stream every unit from HBM / L2 for each
         // pass (exact, any length)
-        hipLaunchKernelGGL(select_stream_kernel<false>, dim3(nseg, ncols), dim3(ST), 0, st, a);
+        hipLaunchKernelGGL(select_stream_kernel, dim3(nseg, ncols), dim3(ST), 0, st, a);
         FM_CHECK_LAUNCH("fm_select_cuts(stream)");
+        launch_fixup(a, max_seg_len, st);
+        FM_CHECK_LAUNCH("fm_select_cuts(stream fix-up)");
         return a.level ? fm_universe_level(cols, seg_off, nseg, (int64_t)max_seg_len * nseg, x.lo, x.hi, x.level, stream) : FM_OK;
     }
     // wave fast path: no row mask, segments of <= 96 * 64 rows, nvalid present (it carries
@@ -1534,23 +1999,17 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
         else launch_select_wave<96>(a, st);
         FM_CHECK_LAUNCH("fm_select_cuts(wave)");
     }
-#ifdef FM_SELECT_DIAG_NO_FALLBACK
-    // diagnostic builds only (-DFM_SELECT_DIAG_NO_FALLBACK, tools/select_marks.py): leave the
-    // wave kernel's fallback marks (nvalid == -1) in place; results are then incomplete.
-    // The shipped library is never built with it.
-    if (wave) return FM_OK;
-#endif
-    if (vpt <= 2) launch_select<2>(a, ncols, st, wave);
-    else if (vpt <= 4) launch_select<4>(a, ncols, st, wave);
-    else if (vpt <= 8) launch_select<8>(a, ncols, st, wave);
-    else if (vpt <= 16) launch_select<16>(a, ncols, st, wave);
-    else if (vpt <= 20) launch_select<20>(a, ncols, st, wave);
-    else if (vpt <= 24) launch_select<24>(a, ncols, st, wave);
-    else if (vpt <= 32) launch_select<32>(a, ncols, st, wave);
-    else if (vpt <= 48) launch_select<48>(a, ncols, st, wave);
-    else if (vpt <= 64) launch_select<64>(a, ncols, st, wave);
-    else launch_select<96>(a, ncols, st, wave);
-    FM_CHECK_LAUNCH("fm_select_cuts");
+    if (!wave) {   // one workgroup per unit (row masks, moments past the wave kernels)
+        if (vpt <= 2) launch_select<2>(a, ncols, st);
+        else if (vpt <= 4) launch_select<4>(a, ncols, st);
+        else if (vpt <= 8) launch_select<8>(a, ncols, st);
+        else if (vpt <= 16) launch_select<16>(a, ncols, st);
+        else if (vpt <= 20) launch_select<20>(a, ncols, st);
+        else launch_select<FM_SELECT_STREAM_VPT>(a, ncols, st);
+        FM_CHECK_LAUNCH("fm_select_cuts");
+    }
+    launch_fixup(a, max_seg_len, st);
+    FM_CHECK_LAUNCH("fm_select_cuts(fix-up)");
     return a.level ? fm_universe_level(cols, seg_off, nseg, (int64_t)max_seg_len * nseg, x.lo, x.hi, x.level, stream) : FM_OK;
 }
 

@@ -28,6 +28,15 @@ constexpr int CAND_CAP = 2048;
 constexpr int HB = 2048;     // hist_select: bins per level
 constexpr int HCAP = 256;    // hist_select: keys per candidate list (one wave sorts them)
 
+// fm_select_args.ws header (zeroed by the caller once; every fm_select leaves it zeroed):
+// the worklist of units the fix-up kernel redoes exactly.
+struct SelCtl {
+    uint32_t nwork;   // worklist length
+    uint32_t done;    // fix-up workgroups finished (the last one resets both)
+    uint32_t pad[62];
+    uint32_t work[1];   // [nseg * ncols] unit ids (column * nseg + month)
+};
+
 // Shared scratch of the workgroup select paths for NW-wave workgroups.
 template <int NW>
 struct SelSmemT {
@@ -68,7 +77,32 @@ struct SelArgs {
     double* ucut_a = nullptr;
     double* ucut_b = nullptr;
     uint8_t* ulevel = nullptr;
+    // fm_select_args.ws: the fix-up worklist (units a fast kernel could not finish, and units
+    // whose numpy cut is exactly zero); NULL inside the fix-up kernel itself
+    SelCtl* ctl = nullptr;
+    // fm_select_args.hi_plane: the columns' high 32-bit words ([ncols][pstride]); the two-wave
+    // and long-month kernels then read 4 bytes per value
+    const uint32_t* hp = nullptr;
+    int64_t pstride = 0;
 };
+
+// One lane: unit u goes on the fix-up kernel's worklist (and is marked, nvalid = -1, when the
+// kernel could not finish it).
+__device__ __forceinline__ void sel_push(const SelArgs& a, int64_t u) {
+    if (a.ctl != nullptr) {
+        const uint32_t i = atomicAdd(&a.ctl->nwork, 1u);
+        a.ctl->work[i] = (uint32_t)u;
+    }
+}
+__device__ __forceinline__ void sel_mark(const SelArgs& a, int64_t u) {
+    if (a.nvalid) a.nvalid[u] = -1;
+    sel_push(a, u);
+}
+// A numpy cut that is exactly +-0: its sign is numpy's partition order's business (the
+// fix-up kernel replays it when the unit holds both signed zeros)
+__device__ __forceinline__ bool zero_cut(const SelArgs& a, double lo, double hi) {
+    return a.lerp_mode == 0 && a.ctl != nullptr && (lo == 0.0 || hi == 0.0);
+}
 
 __device__ __forceinline__ uint64_t key_of(double x) { return isnan(x) ? SENT : dkey(x); }
 
@@ -719,7 +753,7 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
         const bool fast = select_tails<VPT, NW>(xv, mn, mx, n, i0, j0, i1, j1, k0, k1, k2, k3, sm);
         if (MARK && !fast) {
             // MARK: the rare unit the tail path cannot finish is redone by a fallback pass
-            if (threadIdx.x == 0) a.nvalid[(int64_t)c * a.nseg + s] = -1;
+            if (threadIdx.x == 0) sel_mark(a, (int64_t)c * a.nseg + s);
             return;
         }
         if (!MARK && !fast) {
@@ -794,6 +828,7 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
         a.lo[o] = lo;
         a.hi[o] = hi;
         if (a.nvalid) a.nvalid[o] = n;
+        if (zero_cut(a, lo, hi)) sel_push(a, o);
         if (a.prm) {
             a.prm[c] = lo;
             a.prm[32 + c] = hi;

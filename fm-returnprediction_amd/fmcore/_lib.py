@@ -50,7 +50,8 @@ class SelectArgs(C.Structure):
         ("cols", _p), ("col_stride", _i64), ("ncols", _i32), ("seg_off", _p), ("nseg", _i32),
         ("max_seg_len", _i32), ("row_mask", _p), ("q_lo", _f64), ("q_hi", _f64),
         ("min_count", _i32), ("lerp_mode", _i32), ("lo", _p), ("hi", _p), ("nvalid", _p),
-        ("mean", _p), ("sd", _p), ("center", _p), ("level", _p),
+        ("mean", _p), ("sd", _p), ("center", _p), ("level", _p), ("ws", _p),
+        ("hi_plane", _p), ("plane_stride", _i64),
     ]
 
 
@@ -97,8 +98,11 @@ _SIGS = {
     "fm_last_error": (C.c_char_p, []),
     "fm_device_arch": (_i32, [C.c_char_p, _i32]),
     "fm_abi_sizes": (_i32, [C.POINTER(_i32), C.POINTER(_i32)]),
+    "fm_struct_size": (_i64, [C.c_char_p]),
     "fm_select_cuts": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p, _f64, _f64, _i32, _i32,
-                              _p, _p, _p, _p, _p, _p]),
+                              _p, _p, _p, _p, _p, _p, _p]),
+    "fm_select_ws_bytes": (_i64, [_i32, _i32, _i32]),
+    "fm_split_planes": (_i32, [_p, _i64, _i32, _i64, _p, _p, _i64, _p]),
     "fm_select": (_i32, [C.POINTER(SelectArgs), _p]),
     "fm_select_universe": (_i32, [C.POINTER(SelectArgs), C.POINTER(UniverseArgs), _p]),
     "fm_clip": (_i32, [_p, _p, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
@@ -133,6 +137,8 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
+_STRUCTS = {"fm_gram_args": GramArgs, "fm_solve_args": SolveArgs, "fm_select_args": SelectArgs,
+            "fm_universe_args": UniverseArgs, "fm_ts_args": TsArgs, "fm_chars_args": CharsArgs}
 
 _lib = None
 
@@ -155,6 +161,13 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # the argument structs must match the library's layouts byte for byte (a struct shorter
+    # than the C one leaves the library reading past it)
+    for cname, cls in _STRUCTS.items():
+        want = lib.fm_struct_size(cname.encode())
+        if want != C.sizeof(cls):
+            raise ImportError(f"ABI mismatch: {cname} is {want} bytes in libfm_hip.so, "
+                              f"{C.sizeof(cls)} in fmcore._lib.{cls.__name__}")
     _lib = lib
     return lib
 

@@ -216,6 +216,27 @@ class Cuts:
     center: Optional[torch.Tensor] = None   # Gram pivot (midpoint of the cuts)
 
 
+_SELECT_WS = {}   # device -> the zeroed fm_select work buffer (the library leaves it zeroed)
+_SELECT_WS_OLD = []   # outgrown buffers stay alive: captured HIP graphs may still use them
+
+
+def select_ws(nseg, ncols, max_seg_len, device):
+    """fm_select_args.ws: the fix-up worklist (+ zero-sign replay slots for > 6,144-row
+    months), zeroed once; every fm_select call leaves it zeroed, so one buffer per device
+    serves all calls on the stream (grown on demand, never freed while graphs may use it)."""
+    need = int(L.load().fm_select_ws_bytes(int(nseg), int(ncols), int(max_seg_len)))
+    if need < 0:
+        raise ValueError("fm_select_ws_bytes: bad sizes")
+    key = str(device)
+    buf = _SELECT_WS.get(key)
+    if buf is None or buf.numel() < need:
+        if buf is not None:
+            _SELECT_WS_OLD.append(buf)
+        buf = torch.zeros(max(need, 1 << 16), dtype=torch.uint8, device=device)
+        _SELECT_WS[key] = buf
+    return buf
+
+
 def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols=None,
                 row_mask=None, moments=False, center=False, level=None, tag="fm_select_cuts",
                 universe=None):
@@ -239,11 +260,13 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
         sd = torch.empty_like(lo)
     if center:
         cen = torch.empty_like(lo)
+    msl = max(panel.max_seg_len, 1)
+    ws = select_ws(T, C, msl, dev)
     sa = L.SelectArgs(cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, seg_off=panel.seg_off.data_ptr(),
-                      nseg=T, max_seg_len=max(panel.max_seg_len, 1), row_mask=_ptr(row_mask), q_lo=float(q_lo),
+                      nseg=T, max_seg_len=msl, row_mask=_ptr(row_mask), q_lo=float(q_lo),
                       q_hi=float(q_hi), min_count=int(min_count), lerp_mode=int(mode), lo=lo.data_ptr(),
                       hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=_ptr(mean), sd=_ptr(sd), center=_ptr(cen),
-                      level=_ptr(level))
+                      level=_ptr(level), ws=ws.data_ptr())
     if universe is None:
         _kcall(tag, "fm_select", L.C.byref(sa), _stream())
         _remember(tag, "fm_select", sa, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, level)

@@ -153,13 +153,23 @@ typedef struct fm_solve_args {
 const char* fm_version(void);
 const char* fm_last_error(void);
 int fm_abi_sizes(int32_t* gram_args, int32_t* solve_args);
+/* sizeof the named argument struct ("fm_gram_args", "fm_solve_args", "fm_select_args",
+ * "fm_universe_args", "fm_ts_args", "fm_chars_args"); -1 for an unknown name.  Bindings
+ * check their struct layouts against it before the first call. */
+int64_t fm_struct_size(const char* name);
 int fm_device_arch(char* buf, int32_t len);
 
 int fm_select_cuts(const double* cols, int64_t col_stride, int32_t ncols,
                    const int64_t* seg_off, int32_t nseg, int32_t max_seg_len,
                    const uint8_t* row_mask, double q_lo, double q_hi, int32_t min_count,
                    int32_t lerp_mode, double* lo, double* hi, int32_t* nvalid,
-                   double* mean, double* sd, void* stream);
+                   double* mean, double* sd, void* ws, void* stream);
+
+/* Bytes of fm_select_args.ws for a call over nseg x ncols units of <= max_seg_len rows (the
+ * fix-up worklist; past 6,144 rows also the zero-sign replay slots).  The caller zeroes the
+ * buffer ONCE; every fm_select / fm_select_cuts / fm_select_universe call leaves it zeroed,
+ * so one buffer serves any number of calls on one stream.  < 0: bad sizes. */
+int64_t fm_select_ws_bytes(int32_t nseg, int32_t ncols, int32_t max_seg_len);
 
 /* fm_select: fm_select_cuts with an argument struct and one more optional output.
  * Outputs are [ncols][nseg]; every output pointer except lo / hi may be NULL.
@@ -167,8 +177,12 @@ int fm_select_cuts(const double* cols, int64_t col_stride, int32_t ncols,
  *   center:   a pivot inside the data for the Gram (midpoint of the cuts, else of the
  *             segment's finite range, else 0); costs nothing beyond the cuts;
  *   level:    the universe level byte of every row from the two cuts (see the field).
- * Without a row mask and for segments of <= 6144 rows, passing nvalid enables the
- * one-wave-per-(segment, column) fast path (nvalid carries its fallback marks). */
+ * nvalid and ws are required.  Every path ends with a fix-up launch that redoes, exactly, the
+ * units the fast kernels could not finish and the units whose numpy cut is exactly +-0: for
+ * those, when the unit holds both -0.0 and +0.0, numpy 1.26.4's partition order is replayed
+ * (np.percentile takes the sign of a zero cut from it; reference :519-524), so the cuts are
+ * bit-exact including that sign.  The struct must be zero-initialized before filling it (new
+ * trailing fields are then NULL / 0). */
 typedef struct fm_select_args {
     const double* cols;
     int64_t col_stride;
@@ -191,6 +205,13 @@ typedef struct fm_select_args {
                                     False), i.e. get_subsets' nested masks from the NYSE cuts
                                     (src/calc_Lewellen_2014.py:95-105), by a streaming
                                     launch after the cuts (same stream) */
+    void* ws;                    /* fm_select_ws_bytes(nseg, ncols, max_seg_len) bytes, zeroed
+                                    once by the caller, left zeroed by every call */
+    const uint32_t* hi_plane;    /* optional: the high 32-bit words of cols ([ncols][plane_stride],
+                                    fm_split_planes).  The two-wave (<= 6,144-row months) and
+                                    long-month kernels then order values by these words (half the
+                                    bytes) and gather full values from cols only at the target ranks */
+    int64_t plane_stride;
 } fm_select_args;
 
 int fm_select(const fm_select_args* args, void* stream);
@@ -401,6 +422,11 @@ int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
                  double nan_rate, double nyse_rate, double* cols, int64_t col_stride,
                  double* me, uint8_t* nyse, void* stream);
 
+/* The FP64 columns as two 32-bit planes: hi[c][r] / lo[c][r] = the high / low words of
+ * cols[c][r] (plane_stride >= nrows).  The split panel's hi plane feeds fm_select_args.hi_plane
+ * and, with the lo plane, fm_gram_args.hi_plane / lo_plane. */
+int fm_split_planes(const double* cols, int64_t col_stride, int32_t ncols, int64_t nrows, uint32_t* hi,
+                    uint32_t* lo, int64_t plane_stride, void* stream);
 int fm_stream_probe(const double* src, int64_t n, double* out, void* stream);
 
 /* fm_ffill_expand: records sorted by (group, month code) with CSR rec_off[ngroups+1];

@@ -51,12 +51,22 @@ def percentile_linear(vals, pct):
         j = i + 1
         g = vi - np.float64(i)
     a, b = s[i], s[j]
+    if (a == 0.0 or b == 0.0) and _both_zero_signs(s):
+        # -0.0 == +0.0: which signed zero numpy leaves at i / i+1 is its partition's swap
+        # order over the values in frame order (oracle/np_select.py), not the sorted order
+        from oracle import np_select
+        a, b = np_select.percentile_pair(vals, i if vi < n - 1 else -1)
     with np.errstate(invalid="ignore"):
         d = b - a
     with np.errstate(invalid="ignore"):
         if g >= 0.5:
             return float(b - d * (np.float64(1) - g))
         return float(a + d * g)
+
+
+def _both_zero_signs(s):
+    z = s[s == 0.0]
+    return z.size > 1 and np.signbit(z).any() and not np.signbit(z).all()
 
 
 def pandas_quantile(vals, q):
