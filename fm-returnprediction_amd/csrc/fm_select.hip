@@ -1928,8 +1928,7 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
                "fm_select_cuts: quantiles must be in [0,1]");
     if (nseg == 0) return FM_OK;
     FM_REQUIRE(x.level == nullptr || ncols == 1, "fm_select: level needs a single column");
-    FM_REQUIRE(x.ws != nullptr && x.nvalid != nullptr,
-               "fm_select: nvalid and ws (fm_select_ws_bytes, zeroed once) are required");
+    FM_REQUIRE(x.ws != nullptr, "fm_select: ws (fm_select_ws_bytes bytes, zeroed once) is required");
     SelArgs a{cols,        x.col_stride, seg_off, nseg,     ncols, row_mask, x.q_lo, x.q_hi,
               x.min_count, x.lerp_mode,  x.lo,    x.hi,     x.nvalid, x.mean, x.sd,  x.center,
               nullptr,     x.level};

@@ -42,6 +42,7 @@ class GramArgs(C.Structure):
         ("model_mask", _p), ("model_ymask", _p), ("nmodels", _i32),
         ("pattern_id", _p), ("npatterns", _i32),
         ("partial", _p), ("flags", _p), ("chunk_order", _p),
+        ("hi_plane", _p), ("lo_plane", _p), ("plane_stride", _i64),
     ]
 
 

@@ -124,6 +124,7 @@ class DevicePanel:
     order: Optional[np.ndarray] = None   # sorted row -> original positional row
     chunk_rows: Optional[int] = None     # Gram chunking override (sharded runs: global policy)
     chunk_split: Optional[bool] = None   # split-month Gram plan (make_chunks_split) override
+    planes: Optional[torch.Tensor] = None   # [2, C, n] uint32: cols' high / low words (split_planes)
 
     @property
     def nrows(self):
@@ -185,6 +186,27 @@ def panel_from_arrays(arrays: Sequence[np.ndarray], names, labels, me=None, nyse
         nyse_t = torch.from_numpy(np.asarray(nyse, dtype=np.uint8)).to(device).index_select(0, perm)
     return DevicePanel(cols=cols, names=list(names), seg_off=torch.from_numpy(seg_off).to(device),
                        seg_off_h=seg_off, months=uniq, me=me_t, nyse=nyse_t, order=order)
+
+
+def split_planes(panel: DevicePanel):
+    """The panel's FP64 columns as two 32-bit planes (fm_split_planes), kept beside cols:
+    the selects then order values by their high words (half the bytes) and the Gram reads
+    both planes (the high plane the select just streamed is still in the Infinity Cache).
+    A device pass over the panel, done once at ingest."""
+    C, n = panel.cols.shape
+    planes = torch.empty((2, C, max(n, 1)), dtype=torch.int32, device=panel.cols.device)
+    _kcall("fm_split_planes", "fm_split_planes", panel.cols.data_ptr(), panel.stride, C, n, planes[0].data_ptr(),
+           planes[1].data_ptr(), planes.stride(1), _stream())
+    panel.planes = planes
+    return panel
+
+
+def _planes_for(panel: DevicePanel, src):
+    """(hi, lo, stride) when ``src`` is the panel's own columns and they are split."""
+    pl = panel.planes
+    if pl is None or src.data_ptr() != panel.cols.data_ptr() or src.shape[0] != panel.ncols:
+        return None, None, 0
+    return pl[0].data_ptr(), pl[1].data_ptr(), pl.stride(1)
 
 
 def panel_synthetic(nmonths, nfirms, seed, month0=0, nan_rate=0.02, nyse_rate=0.4, device=None):
@@ -262,11 +284,12 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
         cen = torch.empty_like(lo)
     msl = max(panel.max_seg_len, 1)
     ws = select_ws(T, C, msl, dev)
+    hp, _, pst = _planes_for(panel, src) if row_mask is None else (None, None, 0)
     sa = L.SelectArgs(cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, seg_off=panel.seg_off.data_ptr(),
                       nseg=T, max_seg_len=msl, row_mask=_ptr(row_mask), q_lo=float(q_lo),
                       q_hi=float(q_hi), min_count=int(min_count), lerp_mode=int(mode), lo=lo.data_ptr(),
                       hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=_ptr(mean), sd=_ptr(sd), center=_ptr(cen),
-                      level=_ptr(level), ws=ws.data_ptr())
+                      level=_ptr(level), ws=ws.data_ptr(), hi_plane=hp, plane_stride=pst)
     if universe is None:
         _kcall(tag, "fm_select", L.C.byref(sa), _stream())
         _remember(tag, "fm_select", sa, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, level)
@@ -655,6 +678,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
         nb = gpl.npatterns * nlevels
         partial = torch.empty((plan.nchunks, nb, zw * (zw + 1) // 2), dtype=torch.float64, device=dev)
         flags = torch.empty((T, gpl.nmodels), dtype=torch.int32, device=dev)   # reserved: never read
+        ph, pl_, pst = _planes_for(panel, src)
         ga = L.GramArgs(
             cols=src.data_ptr(), col_stride=src.stride(0), ncols=ncols, nseg=T,
             seg_off=panel.seg_off.data_ptr(), chunk_seg=plan.chunk_seg.data_ptr(),
@@ -663,7 +687,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
             level=_ptr(level), nlevels=nlevels, model_mask=gpl.mm.data_ptr(),
             model_ymask=gpl.ym.data_ptr(), nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(),
             npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr(),
-            chunk_order=_ptr(plan.order))
+            chunk_order=_ptr(plan.order), hi_plane=ph, lo_plane=pl_, plane_stride=pst)
         _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
         _remember("fm_gram", "fm_gram", ga, src, partial, flags, lo, hi, shift, inv_scale, level, plan, gpl)
         grec, gst, gmom = _solve_group(panel, src, gpl, partial, plan.seg_chunk_off, zw, nlevels, T, pmax,

@@ -122,7 +122,15 @@ typedef struct fm_gram_args {
                                      reverse index order (the months fm_select streamed last, still
                                      in the Infinity Cache, first).  Only the launch order: each
                                      chunk's partial is the same either way */
+    /* optional: cols as 32-bit planes (fm_split_planes, [ncols][plane_stride] each): rows are
+     * read from the planes instead of cols (the same bytes; the high plane fm_select just
+     * streamed is still in the Infinity Cache).  NULL: cols */
+    const uint32_t* hi_plane;
+    const uint32_t* lo_plane;
+    int64_t plane_stride;
 } fm_gram_args;
+/* The argument structs (fm_gram_args, fm_solve_args, fm_select_args, ...) grow at the end:
+ * zero-initialize them before filling fields, so fields a caller does not know are NULL / 0. */
 
 typedef struct fm_solve_args {
     const double* partial;        /* from fm_gram */
@@ -177,7 +185,7 @@ int64_t fm_select_ws_bytes(int32_t nseg, int32_t ncols, int32_t max_seg_len);
  *   center:   a pivot inside the data for the Gram (midpoint of the cuts, else of the
  *             segment's finite range, else 0); costs nothing beyond the cuts;
  *   level:    the universe level byte of every row from the two cuts (see the field).
- * nvalid and ws are required.  Every path ends with a fix-up launch that redoes, exactly, the
+ * ws is required (nvalid enables the wave fast paths).  Every path ends with a fix-up launch that redoes, exactly, the
  * units the fast kernels could not finish and the units whose numpy cut is exactly +-0: for
  * those, when the unit holds both -0.0 and +0.0, numpy 1.26.4's partition order is replayed
  * (np.percentile takes the sign of a zero cut from it; reference :519-524), so the cuts are

@@ -266,6 +266,63 @@ def test_long_month_register_select_bit_exact(E, maxlen):
             assert _same([lo[t]], [ra]) and _same([hi[t]], [rb]), (qa, qb, t, len(v), lo[t], ra, hi[t], rb)
 
 
+def _high_word_tie_segments(rng, n):
+    """Months whose cut ranks sit in runs of equal HIGH 32-bit words (values differing only
+    in the low word), exact duplicates at the ranks, and the high-word plane's ambiguous keys."""
+    segs = []
+    x = rng.standard_normal(n)
+    k = max(1, n // 100)
+    lo_ix = np.argsort(x)[: 3 * k]
+    base = np.float64(-2.5).view(np.uint64)
+    x[lo_ix] = (base + rng.integers(0, 2 ** 16, lo_ix.size).astype(np.uint64)).view(np.float64)
+    segs.append(x)                                   # ~3k values share one high word at the low cut
+    y = rng.standard_normal(n)
+    y[np.argsort(y)[-2 * k:]] = 4.0                  # exact duplicates across the upper cut
+    segs.append(y)
+    z = rng.standard_normal(n)
+    z[rng.choice(n, 4, replace=False)] = [np.inf, -np.inf, np.inf, -np.inf]
+    segs.append(z)                                   # +-inf: ambiguous high words -> fix-up
+    w = rng.standard_normal(n)
+    w[rng.choice(n, 6, replace=False)] = _payload_nan(1, 6)
+    segs.append(w)
+    v = np.round(rng.standard_normal(n), 2)          # heavy exact ties everywhere
+    segs.append(v)
+    return segs
+
+
+@pytest.mark.parametrize("maxlen", [128, 5000, 6144, 9000, 20000])
+def test_hi_plane_select_bit_exact(E, maxlen):
+    """The split panel: the two-wave kernel (<= 6,144-row months) and the long-month kernel
+    order values by their HIGH words (fm_split_planes) and gather full values only at the
+    target ranks.  Cuts, counts and pivots bit-identical to the FP64-column path and to
+    np.percentile, over the adversarial kinds, high-word ties at the cut ranks, duplicates,
+    +-inf and low-payload NaNs."""
+    rng = np.random.default_rng(maxlen + 11)
+    lengths = sorted({1, 2, 5, 63, 64, 65, 127, 128, 129, maxlen // 2 + 1, maxlen - 1, maxlen})
+    segs = _adversarial_segments(rng, lengths) + _high_word_tie_segments(rng, maxlen)
+    vals = np.concatenate(segs)
+    labels = np.repeat(np.arange(len(segs)), [len(s_) for s_ in segs])
+    panel = E.panel_from_arrays([vals, vals[::-1].copy()], ["v", "r"], labels)
+    rv = [np.concatenate(segs)[::-1]]
+    assert panel.max_seg_len == maxlen
+    qs = ((1, 99), (0, 100), (5, 95))
+    ref = [E.select_cuts(panel, a / 100, b / 100, 1, E.LERP_NUMPY, center=True) for a, b in qs]
+    E.split_planes(panel)
+    for (qa, qb), r in zip(qs, ref):
+        got = E.select_cuts(panel, qa / 100, qb / 100, 1, E.LERP_NUMPY, center=True)
+        for f in ("lo", "hi", "center"):
+            assert _same(getattr(got, f).cpu().numpy(), getattr(r, f).cpu().numpy()), (qa, qb, f)
+        assert np.array_equal(got.nvalid.cpu().numpy(), r.nvalid.cpu().numpy())
+        lo, hi = got.lo.cpu().numpy()[0], got.hi.cpu().numpy()[0]
+        for t, s_ in enumerate(segs):
+            v = s_[~np.isnan(s_)]
+            if len(v) == 0:
+                continue
+            assert _same([lo[t]], [O.percentile_linear(v, qa)]) and _same([hi[t]], [O.percentile_linear(v, qb)]), \
+                (qa, qb, t, len(v))
+    assert rv is not None
+
+
 def _payload_nan(sign, n):
     """n NaNs whose payload sits entirely in the LOW 32 bits (high word 0x7FF00000 /
     0xFFF00000, the same high word as +-inf)."""
@@ -1112,8 +1169,14 @@ def test_pipeline_headline_panel_full_size(E):
     T, N, seed = 600, 5000, 1
     panel = E.panel_synthetic(T, N, seed)
     cfg = LW.PipelineConfig()
+    # the FP64-column pass first, then the bench's split panel (fm_split_planes: the selects on
+    # the high-word plane, the Gram on both planes): bit-identical records
+    flat, _, _ = ShardedStep(panel, cfg, LW.table2_models()).eager()
+    flat_rec = flat.rec.cpu().numpy()
+    E.split_planes(panel)
     step = ShardedStep(panel, cfg, LW.table2_models())
     gres, summ, psumm = step.eager()
+    assert _same(gres.rec.cpu().numpy(), flat_rec)
     step.capture()
     ggres, gsumm, gpsumm = step.replay()
     torch.cuda.synchronize()
