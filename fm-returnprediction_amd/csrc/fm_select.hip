@@ -1365,9 +1365,14 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
 //   4. wave t sorts tail t's candidates by (key, row) and gathers the FP64 values at the two
 //      target ranks from the column (4 scattered loads per unit); when high words tie at those
 //      ranks every tied candidate is gathered and the tie broken by the full keys.
+// resident two-wave workgroups per CU (the register budget and the persistent grid): the keys
+// take VPH VGPRs beside ~70 for the rest (the next unit's keys are in flight during the pick)
 #ifndef FM_PAIR_HK_WGS
-#define FM_PAIR_HK_WGS 12   // resident two-wave workgroups per CU (register budget and grid)
+#define FM_PAIR_HK_WGS 0   // 0: by VPH
 #endif
+constexpr int pair_hk_wgs(int vph) {
+    return FM_PAIR_HK_WGS > 0 ? FM_PAIR_HK_WGS : (vph <= 16 ? 12 : (vph <= 24 ? 10 : 8));
+}
 struct PairHkSmem {
     uint32_t sk[2][2][WAVE];     // [wave][lo / hi][lane] sorted lane-extreme keys
     uint64_t cand[2][2][WCAP];   // [wave][lo / hi] (key << 32 | row) candidates
@@ -1456,7 +1461,7 @@ __device__ __forceinline__ bool pick_hk(uint64_t* L1, int c1, const uint64_t* L2
 }
 
 template <int VPH>
-__global__ __launch_bounds__(2 * WAVE, FM_PAIR_HK_WGS / 2) void select_pair_hk_kernel(SelArgs a) {
+__global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk_kernel(SelArgs a) {
     __shared__ PairHkSmem sm;
     const int lane = lane_id();
     const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
@@ -1703,7 +1708,7 @@ void launch_select_pair_hk(const SelArgs& a, hipStream_t st) {
         return n;
     }();
     const int64_t nunits = (int64_t)a.nseg * a.ncols;
-    const int64_t cap = (int64_t)ncu * FM_PAIR_HK_WGS;
+    const int64_t cap = (int64_t)ncu * pair_hk_wgs(VPH);
     hipLaunchKernelGGL((select_pair_hk_kernel<VPH>), dim3((unsigned)(nunits < cap ? nunits : cap)), dim3(2 * WAVE),
                        0, st, a);
 }
