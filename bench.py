@@ -180,8 +180,10 @@ def make_step(T_loc, N, seed, world, rank, dev, E, LW, planes=True):
     panel.ingest_ms = split_ingest(panel, E, planes)
     T_glob = T_loc * world
     # chunk the Gram by the GLOBAL panel so per-month sums are identical for any rank count
-    panel.chunk_rows = E.default_chunk_rows(T_glob * N, T_glob, N)
-    panel.chunk_split = E.split_policy(T_glob)
+    # one Gram plan for every rank (equal shards: the same policy), cut in GLOBAL row space, so
+    # a month's sums do not depend on the rank count
+    panel.chunk_policy = E.chunk_policy(T_loc * N, T_loc, N)
+    panel.row_origin = rank * T_loc * N
     step = ShardedStep(panel, LW.PipelineConfig(), LW.table2_models(), world=world, rank=rank,
                        seg_lo=rank * T_loc, seg_hi=(rank + 1) * T_loc, global_months=T_glob,
                        counts=[T_loc] * world)

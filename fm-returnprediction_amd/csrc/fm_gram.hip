@@ -41,47 +41,59 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);   // wave-uniform (SGPR loops)
-    // default order last-month-first: fm_select streams the panel month by month, so the
-    // months it read last are still in the memory-side cache when they are read here; with
-    // a chunk_order (the split-month plan) the big chunks go first, the small ones fill in
-    const int chunk = a.chunk_order ? a.chunk_order[blockIdx.x] : (int)gridDim.x - 1 - (int)blockIdx.x;
-    const int seg = a.chunk_seg[chunk];
-    const int64_t r0 = a.chunk_row[2 * chunk], r1 = a.chunk_row[2 * chunk + 1];
     const int ncols = a.ncols, nseg = a.nseg;
-
-    // Prologue loads (month parameters, pattern table) are unconditional (pointer/index
-    // selected, value masked after) and issued before the first tile's row loads, so
-    // waiting for them does not wait for the tile.
-    double pv;
-    int lutv;
-    {
-        const int kind = tid >> 5, c = tid & 31;
-        const double* src = kind == 0 ? a.lo : kind == 1 ? a.hi : kind == 2 ? a.shift : a.inv_scale;
-        const bool on = tid < 128 && c < ncols && src != nullptr;
-        const double* pp = on ? src + (int64_t)c * nseg + seg : a.cols;
-        const double v = *pp;
-        const double dflt = kind < 2 ? NAN : (kind == 2 ? 0.0 : 1.0);
-        pv = on ? v : dflt;
-        const int npat = 1 << a.nmodels;
-        lutv = a.pattern_id[tid < npat ? tid : 0];
-    }
-    GramWave<NT, NB, GNW, PL> g(a, r0, r1, w);
-    g.prefetch();
-    for (int e = tid; e < 4 * S::RS; e += GT) zblk[e] = 0.0;
-    if (tid < 128) prm[tid >> 5][tid & 31] = pv;
-    if (tid < 64) lut[tid] = (uint8_t)lutv;
-    __syncthreads();
-    g.run(prm, lut, a.inv_scale != nullptr, tile, zblk);
     const int nbr = a.npatterns * a.nlevels;
-    g.epilogue(tile, a.partial + (int64_t)chunk * nbr * S::PK, nbr);
+    // default order last-first: fm_select streams the panel month by month, so the months it
+    // read last are still in the memory-side cache when they are read here; with a
+    // chunk_order (the split-month plan) the big chunks go first, the small ones fill in; with
+    // a balanced plan (wg_chunk_off) workgroup b takes its run of consecutive chunks
+    int c0, c1;
+    if (a.wg_chunk_off != nullptr) {
+        const int b = (int)gridDim.x - 1 - (int)blockIdx.x;
+        c0 = a.wg_chunk_off[b];
+        c1 = a.wg_chunk_off[b + 1];
+    } else {
+        c0 = a.chunk_order ? a.chunk_order[blockIdx.x] : (int)gridDim.x - 1 - (int)blockIdx.x;
+        c1 = c0 + 1;
+    }
+    const int npat = 1 << a.nmodels;
+    const int lutv = a.pattern_id[tid < npat ? tid : 0];
+    for (int chunk = c0; chunk < c1; ++chunk) {
+        const int seg = a.chunk_seg[chunk];
+        const int64_t r0 = a.chunk_row[2 * chunk], r1 = a.chunk_row[2 * chunk + 1];
+        // Prologue loads (month parameters) are unconditional (pointer/index selected, value
+        // masked after) and issued before the first tile's row loads, so waiting for them does
+        // not wait for the tile.
+        double pv;
+        {
+            const int kind = tid >> 5, c = tid & 31;
+            const double* src = kind == 0 ? a.lo : kind == 1 ? a.hi : kind == 2 ? a.shift : a.inv_scale;
+            const bool on = tid < 128 && c < ncols && src != nullptr;
+            const double* pp = on ? src + (int64_t)c * nseg + seg : a.cols;
+            const double v = *pp;
+            const double dflt = kind < 2 ? NAN : (kind == 2 ? 0.0 : 1.0);
+            pv = on ? v : dflt;
+        }
+        GramWave<NT, NB, GNW, PL> g(a, r0, r1, w);
+        g.prefetch();
+        if (chunk == c0) {
+            for (int e = tid; e < 4 * S::RS; e += GT) zblk[e] = 0.0;
+            if (tid < 64) lut[tid] = (uint8_t)lutv;
+        }
+        if (tid < 128) prm[tid >> 5][tid & 31] = pv;   // the previous chunk's epilogue ended in a barrier
+        __syncthreads();
+        g.run(prm, lut, a.inv_scale != nullptr, tile, zblk);
+        g.epilogue(tile, a.partial + (int64_t)chunk * nbr * S::PK, nbr);
+    }
 }
 
 template <int NT, int NB, int MINW>
 void launch_gram(const fm_gram_args& a, hipStream_t st) {
+    const int grid = a.wg_chunk_off != nullptr ? a.nwg : a.nchunks;
     if (a.hi_plane != nullptr)
-        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true>), dim3(a.nchunks), dim3(GT), 0, st, a);
+        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true>), dim3(grid), dim3(GT), 0, st, a);
     else
-        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false>), dim3(a.nchunks), dim3(GT), 0, st, a);
+        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false>), dim3(grid), dim3(GT), 0, st, a);
 }
 
 }  // namespace
@@ -103,6 +115,8 @@ extern "C" int fm_gram(const fm_gram_args* args, void* stream) {
                FM_MAX_LEVELS);
     FM_REQUIRE(a.npatterns >= 1, "fm_gram: npatterns must be >= 1");
     if (a.nchunks == 0) return FM_OK;
+    FM_REQUIRE(a.wg_chunk_off == nullptr || (a.nwg >= 1 && a.chunk_order == nullptr),
+               "fm_gram: a balanced plan needs nwg >= 1 and no chunk_order");
     const int nb = a.npatterns * a.nlevels;
     hipStream_t st = (hipStream_t)stream;
     if (a.ncols <= 15) {

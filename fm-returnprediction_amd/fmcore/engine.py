@@ -125,6 +125,8 @@ class DevicePanel:
     chunk_rows: Optional[int] = None     # Gram chunking override (sharded runs: global policy)
     chunk_split: Optional[bool] = None   # split-month Gram plan (make_chunks_split) override
     planes: Optional[torch.Tensor] = None   # [2, C, n] uint32: cols' high / low words (split_planes)
+    chunk_policy: Optional[tuple] = None    # Gram plan of the GLOBAL panel (chunk_policy()), sharded runs
+    row_origin: int = 0                     # global row of this panel's row 0 (balanced plans)
 
     @property
     def nrows(self):
@@ -463,6 +465,69 @@ def default_chunk_rows(total_rows, nseg, max_seg_len, target_chunks=512):
     return max(256, ((ch + 255) // 256) * 256)
 
 
+GRAM_SLOTS_PER_CU = 3   # fm_gram workgroups resident per CU (3 waves / SIMD)
+
+
+def _num_cus():
+    try:
+        return torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    except Exception:
+        return 256
+
+
+def chunk_policy(total_rows, nseg, max_seg_len, slots=None, min_rows=2048):
+    """The Gram's chunk plan for a panel of these GLOBAL sizes (sharded callers pass the
+    global panel's, so every rank cuts, and sums, every month identically):
+
+    * ("balanced", R): when the months are too few to even out over the resident workgroup
+      slots (fewer than 4 rounds of them), every workgroup takes R consecutive rows of the
+      global row space, cut at month boundaries into chunks (a workgroup can end one month and
+      start the next), so every CU gets the same rows.  At the bench's 600 x 5,000 panel a
+      grid of whole months leaves 88 CUs a third month to finish while the rest idle
+      (profiles/r04/v1_size_scan.log: 600 months cost what 768 do).
+    * ("months", chunk_rows): otherwise months split into ceil(L / chunk_rows) chunks
+      (default_chunk_rows), one per workgroup."""
+    slots = slots or _num_cus() * GRAM_SLOTS_PER_CU
+    if nseg > 0 and nseg < 4 * slots:
+        R = -(-int(total_rows) // slots)
+        if R >= min_rows:
+            return ("balanced", int(R))
+    return ("months", default_chunk_rows(total_rows, nseg, max_seg_len))
+
+
+def make_chunks_balanced(seg_off_h, rows_per_wg, row_origin=0):
+    """Chunks = the row space cut at month boundaries and at global row multiples of
+    rows_per_wg (row_origin = global row of local row 0); the chunks of one R-block go to one
+    workgroup.  Returns (seg, rows, off, wg_off): chunk month, (r0, r1) pairs, a month's chunk
+    range (fm_solve sums them in order) and each workgroup's chunk range.  A function of the
+    global row space only, so a month's chunks (and sums) do not depend on the sharding."""
+    so = np.asarray(seg_off_h, dtype=np.int64)
+    T = len(so) - 1
+    total = int(so[-1])
+    R = int(rows_per_wg)
+    first = (-int(row_origin)) % R
+    blk = np.arange(first, total, R, dtype=np.int64)
+    cuts = np.unique(np.concatenate([so, blk[blk > 0]]))
+    starts, ends = cuts[:-1], cuts[1:]
+    seg_of = np.searchsorted(so, starts, side="right") - 1
+    # empty months keep one empty chunk (fm_solve then sums nothing for them)
+    empty = np.nonzero(np.diff(so) == 0)[0]
+    if len(empty):
+        starts = np.concatenate([starts, so[empty]])
+        ends = np.concatenate([ends, so[empty]])
+        seg_of = np.concatenate([seg_of, empty])
+        order = np.lexsort((seg_of, starts))   # by row, then month (an empty month before the next)
+        starts, ends, seg_of = starts[order], ends[order], seg_of[order]
+    seg = seg_of.astype(np.int32)
+    rows = np.stack([starts, ends], axis=1).reshape(-1).astype(np.int64)
+    off = np.zeros(T + 1, dtype=np.int32)
+    np.cumsum(np.bincount(seg, minlength=T), out=off[1:])
+    blk_of = (int(row_origin) + starts) // R
+    brk = np.nonzero(np.diff(blk_of))[0] + 1
+    wg_off = np.concatenate([[0], brk, [len(seg)]]).astype(np.int32)
+    return seg, rows, off, wg_off
+
+
 def split_policy(nseg):
     """Whether the Gram takes the split-month plan (make_chunks_split) by default.  A grid of
     whole months that is a few rounds of the chip's resident workgroup slots leaves the CUs
@@ -527,25 +592,32 @@ class _Plan:
     seg_chunk_off: torch.Tensor
     nchunks: int
     order: Optional[torch.Tensor] = None   # fm_gram launch order (split plan) or None
+    wg_off: Optional[torch.Tensor] = None  # balanced plan: each workgroup's chunk range
+    nwg: int = 0
 
 
 def _chunk_plan(panel: DevicePanel):
     cache = getattr(panel, "_chunk_cache", None)
     if cache is not None:
         return cache
+    pol = panel.chunk_policy
+    if pol is None and panel.chunk_rows is not None:   # a sharded caller's global months policy
+        pol = ("months", panel.chunk_rows)
     split = panel.chunk_split
-    if split is None:   # an explicit chunk_rows (a sharded caller's global policy) keeps it
-        split = panel.chunk_rows is None and split_policy(panel.nseg)
-    order = None
+    if split is None:
+        split = pol is None and split_policy(panel.nseg)
+    if pol is None and not split:
+        pol = chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len)
+    order = wg = None
     if split:
         seg, rows, off, order = make_chunks_split(panel.seg_off_h)
+    elif pol[0] == "balanced":
+        seg, rows, off, wg = make_chunks_balanced(panel.seg_off_h, pol[1], panel.row_origin)
     else:
-        ch = panel.chunk_rows or default_chunk_rows(panel.nrows, panel.nseg, panel.max_seg_len)
-        seg, rows, off = make_chunks(panel.seg_off_h, ch)
+        seg, rows, off = make_chunks(panel.seg_off_h, pol[1])
     dev = panel.cols.device
-    plan = _Plan(torch.from_numpy(seg).to(dev), torch.from_numpy(rows).to(dev),
-                 torch.from_numpy(off).to(dev), len(seg),
-                 None if order is None else torch.from_numpy(order).to(dev))
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    plan = _Plan(t(seg), t(rows), t(off), len(seg), t(order), t(wg), 0 if wg is None else len(wg) - 1)
     panel._chunk_cache = plan
     return plan
 
@@ -687,7 +759,8 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
             level=_ptr(level), nlevels=nlevels, model_mask=gpl.mm.data_ptr(),
             model_ymask=gpl.ym.data_ptr(), nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(),
             npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr(),
-            chunk_order=_ptr(plan.order), hi_plane=ph, lo_plane=pl_, plane_stride=pst)
+            chunk_order=_ptr(plan.order), hi_plane=ph, lo_plane=pl_, plane_stride=pst,
+            wg_chunk_off=_ptr(plan.wg_off), nwg=plan.nwg)
         _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
         _remember("fm_gram", "fm_gram", ga, src, partial, flags, lo, hi, shift, inv_scale, level, plan, gpl)
         grec, gst, gmom = _solve_group(panel, src, gpl, partial, plan.seg_chunk_off, zw, nlevels, T, pmax,

@@ -128,6 +128,12 @@ typedef struct fm_gram_args {
     const uint32_t* hi_plane;
     const uint32_t* lo_plane;
     int64_t plane_stride;
+    /* optional balanced plan: workgroup b accumulates chunks [wg_chunk_off[b], wg_chunk_off[b+1])
+     * one after another (a chunk still lies inside one segment; a workgroup's chunks are
+     * consecutive, so a workgroup can take the tail of one month and the head of the next and
+     * every workgroup gets the same number of rows).  NULL: one chunk per workgroup */
+    const int32_t* wg_chunk_off;
+    int32_t nwg;
 } fm_gram_args;
 /* The argument structs (fm_gram_args, fm_solve_args, fm_select_args, ...) grow at the end:
  * zero-initialize them before filling fields, so fields a caller does not know are NULL / 0. */

@@ -42,7 +42,8 @@ def _run(world, rank, T_loc):
     dev = E.require_device()
     T_glob = T_loc * world
     panel = E.panel_synthetic(T_loc, FIRMS, SEED, month0=rank * T_loc, device=dev)
-    panel.chunk_rows = E.default_chunk_rows(T_glob * FIRMS, T_glob, FIRMS)
+    panel.chunk_policy = E.chunk_policy(T_loc * FIRMS, T_loc, FIRMS)   # as bench.make_step
+    panel.row_origin = rank * T_loc * FIRMS
     step = ShardedStep(panel, LW.PipelineConfig(), LW.table2_models(), world=world, rank=rank,
                        seg_lo=rank * T_loc, seg_hi=(rank + 1) * T_loc, global_months=T_glob,
                        counts=[T_loc] * world)

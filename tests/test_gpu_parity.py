@@ -1010,23 +1010,27 @@ def test_rolling_skips_infinite_coefficients(CL):
     assert np.isfinite(got.values[75:]).all()
 
 
-def test_sharded_pipeline_bit_identical(E):
+@pytest.mark.parametrize("policy", ["default", "balanced"])
+def test_sharded_pipeline_bit_identical(E, policy):
     """SURVEY §8(e) on one GPU: split a ragged panel into 3 month ranges with
-    dist.shard_bounds, run local_stage per range with the GLOBAL chunk policy, concatenate
-    the records, run time_series_stage per shard (global records, local moments, its
-    seg_lo/seg_hi) and SUM the predictive records -- every output must equal the unsharded
-    run_pipeline bit for bit (NaN patterns included)."""
+    dist.shard_bounds, run local_stage per range with the GLOBAL chunk policy (whole-month
+    chunks, or the balanced plan cut in global row space: chunks crossing workgroups
+    mid-month), concatenate the records, run time_series_stage per shard (global records,
+    local moments, its seg_lo/seg_hi) and SUM the predictive records -- every output must
+    equal the unsharded run_pipeline bit for bit (NaN patterns included)."""
     import torch
     from fmcore import dist as D, lewellen as LW, synth
     a = synth.synth_arrays(96, 400, 13, nan_rate=0.03, present_rate=0.6)   # ragged months
     _unfitted_early_months(a)
     cols = list(dict.fromkeys(["retx"] + [c for xs in LW.table2_models().values() for c in xs] + LW.FIG1_VARS))
     panel = E.panel_from_arrays([a[c] for c in cols], cols, a["month"], me=a["me"], nyse=a["nyse"])
+    pol = (E.chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len) if policy == "default"
+           else ("balanced", 997))
+    panel.chunk_policy = pol
     cfg = LW.PipelineConfig()
     mc = LW.table2_models()
     full = LW.run_pipeline(panel, cfg, model_cols=mc)
     off = panel.seg_off_h
-    ch = E.default_chunk_rows(panel.nrows, panel.nseg, panel.max_seg_len)
     bounds = D.shard_bounds(np.diff(off), 3)
     assert len({e - s for s, e in bounds}) > 1
     locs = []
@@ -1036,7 +1040,7 @@ def test_sharded_pipeline_bit_identical(E):
         sub = E.DevicePanel(cols=panel.cols[:, r0:r1].contiguous(), names=panel.names,
                             seg_off=torch.from_numpy(so).to(panel.cols.device), seg_off_h=so,
                             me=panel.me[r0:r1].contiguous(), nyse=panel.nyse[r0:r1].contiguous(),
-                            chunk_rows=ch)
+                            chunk_policy=pol, row_origin=r0)
         locs.append(LW.local_stage(sub, cfg, mc)[0])
     rec = torch.cat([r.rec for r in locs])
     st = torch.cat([r.status for r in locs])
@@ -1554,21 +1558,27 @@ def test_rolling_mean_outlier_months(E, fused):
 
 def test_split_month_gram_plan_matches_whole(E):
     """The split-month Gram plan (each month as a 3/4 + 1/4 chunk pair, big chunks launched
-    first) against whole-month chunks on the same 600-month panel: identical month lists,
-    N and status; params and R2 within 1e-12 of the series scale (only the summation order
-    differs)."""
+    first) and the balanced plan (workgroups of equal row counts cut at month boundaries,
+    workgroups spanning two months) against whole-month chunks on the same 600-month panel:
+    identical month lists, N and status; params and R2 within 1e-12 of the series scale (only
+    the summation order differs)."""
     from fmcore import lewellen as LW
     panel = E.panel_synthetic(600, 1200, 5)
     out = {}
-    for split in (False, True):
-        panel.chunk_split = split
+    for plan in ("months", "split", "balanced"):
+        panel.chunk_split = plan == "split"
+        panel.chunk_policy = {"months": ("months", 1200), "split": None, "balanced": ("balanced", 937)}[plan]
         panel.__dict__.pop("_chunk_cache", None)
         res = LW.local_stage(panel, LW.PipelineConfig(), LW.table2_models())[0]
-        out[split] = (res.rec.cpu().numpy(), res.status.cpu().numpy())
-    assert E._chunk_plan(panel).order is not None
-    (ra, sa), (rb, sb) = out[False], out[True]
-    assert np.array_equal(sa, sb)
-    assert _same(ra[..., -1], rb[..., -1])   # N
-    for k in range(ra.shape[1]):
-        for j in range(ra.shape[2] - 1):
-            assert_series_close(rb[:, k, j], ra[:, k, j], f"problem {k} col {j}", rtol=1e-12)
+        out[plan] = (res.rec.cpu().numpy(), res.status.cpu().numpy())
+        if plan == "balanced":
+            pl = E._chunk_plan(panel)
+            assert pl.nwg == -(-600 * 1200 // 937) and pl.nchunks > pl.nwg
+    ra, sa = out["months"]
+    for plan in ("split", "balanced"):
+        rb, sb = out[plan]
+        assert np.array_equal(sa, sb)
+        assert _same(ra[..., -1], rb[..., -1])   # N
+        for k in range(ra.shape[1]):
+            for j in range(ra.shape[2] - 1):
+                assert_series_close(rb[:, k, j], ra[:, k, j], f"{plan} problem {k} col {j}", rtol=1e-12)

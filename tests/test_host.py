@@ -241,3 +241,38 @@ def test_split_month_chunk_plan():
     nbig = len(lens)
     assert list(order[:nbig]) == list(coff[:-1][::-1])
     assert not split_policy(600) and not split_policy(12500)
+
+
+def test_balanced_chunk_plan():
+    """fm_gram's balanced plan: chunks never straddle a month, a month's chunks are
+    contiguous and cover it (empty months keep one empty chunk), every workgroup's chunks lie
+    in one global R-row block, and the plan of a shard (row_origin) equals the global plan
+    restricted to its months -- so a month sums the same rows in the same order at any
+    rank count."""
+    from fmcore.engine import chunk_policy, make_chunks_balanced
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 9000, 57)
+    lens[[3, 4, 20]] = 0
+    so = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    for R in (997, 3906, 10 ** 6):
+        seg, rows, off, wg = make_chunks_balanced(so, R)
+        r = rows.reshape(-1, 2)
+        assert (np.diff(seg) >= 0).all() and (r[:, 0] <= r[:, 1]).all()
+        for m in range(len(so) - 1):
+            rr = r[off[m]:off[m + 1]]
+            assert len(rr) >= 1 and (seg[off[m]:off[m + 1]] == m).all()
+            assert rr[0, 0] == so[m] and rr[-1, 1] == so[m + 1] and (rr[1:, 0] == rr[:-1, 1]).all()
+        for b in range(len(wg) - 1):
+            nz = r[wg[b]:wg[b + 1]]
+            nz = nz[nz[:, 1] > nz[:, 0]]
+            assert len(set((nz[:, 0] // R).tolist())) <= 1 and ((nz[:, 1] - 1) // R == nz[:, 0] // R).all()
+        # a shard of months [s0, s1) with its global row origin: the same chunks of its months
+        s0, s1 = 10, 40
+        sub = so[s0:s1 + 1] - so[s0]
+        seg2, rows2, off2, _ = make_chunks_balanced(sub, R, row_origin=int(so[s0]))
+        for m in range(s1 - s0):
+            a = r[off[s0 + m]:off[s0 + m + 1]]
+            b = rows2.reshape(-1, 2)[off2[m]:off2[m + 1]] + so[s0]
+            assert np.array_equal(a, b)
+    assert chunk_policy(3_000_000, 600, 5000, slots=768) == ("balanced", 3907)
+    assert chunk_policy(250_000_000, 12500, 20000, slots=768)[0] == "months"
