@@ -129,7 +129,9 @@ __device__ void np_dumb_select(A arr, int b, int num, int kth) {
 template <class A>
 __device__ void np_hoare(A arr, int n, double pv, int& ll, int& hh) {
     const int lane = lane_id();
-    while (true) {
+    // every round swaps >= 1 pair, steps a window past stopper-free positions or ends: the
+    // bound only guards against a hang (tests/test_npsel_batch.py checks the loop on the CPU)
+    for (int it = 0; it < 2 * n + 256; ++it) {
         const int pl = ll + 1 + lane, pr = hh - 1 - lane;
         const double xl = arr.ld(pl < n ? pl : n - 1);
         const double xr = arr.ld(pr >= 0 ? pr : 0);
@@ -289,29 +291,16 @@ __device__ void np_introselect(A arr, int num, int kth, int& piv, int& npiv, boo
 // n - 2, numpy's index -1 for both; kth = [0, n-1]).  Wave-uniform results.
 template <class A>
 __device__ void np_percentile_pair(A arr, int n, int i, double& va, double& vb) {
-    int ks[4], nk = 0;
-    if (i < 0) {
-        ks[nk++] = 0;
-        ks[nk++] = n - 1;
-    } else {
-        // np.unique([0, -1, i, i+1]) -> -1 + n -> sorted (duplicates after the +n kept)
-        int raw[4] = {0, -1, i, i + 1}, u[4], nu = 0;
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            bool dup = false;
-            for (int b = 0; b < nu; ++b) dup = dup || u[b] == raw[a];
-            if (!dup) u[nu++] = raw[a];
-        }
-        for (int a = 0; a < nu; ++a) ks[nk++] = u[a] < 0 ? u[a] + n : u[a];
-        for (int a = 1; a < nk; ++a)   // insertion sort
-            for (int b = a; b > 0 && ks[b - 1] > ks[b]; --b) {
-                const int t = ks[b];
-                ks[b] = ks[b - 1];
-                ks[b - 1] = t;
-            }
-    }
+    // kth = np.unique([0, -1, i, i+1]) made non-negative and sorted: [0, i (i > 0), i+1, n-1]
+    // (i+1 == n-1 stays a duplicate: its second introselect finds the pivot and returns);
+    // the rank past n - 2 (i < 0): [0, n-1].  Straight-line: no private arrays.
     int piv = 0, npiv = 0;
-    for (int k = 0; k < nk; ++k) np_introselect<4>(arr, n, ks[k], piv, npiv, true);
+    np_introselect<4>(arr, n, 0, piv, npiv, true);
+    if (i >= 0) {
+        if (i > 0) np_introselect<4>(arr, n, i, piv, npiv, true);
+        np_introselect<4>(arr, n, i + 1, piv, npiv, true);
+    }
+    np_introselect<4>(arr, n, n - 1, piv, npiv, true);
     arr.sync();
     const int ia = i < 0 ? n - 1 : i, ib = i < 0 ? n - 1 : i + 1;
     va = arr.ld(ia);

@@ -1370,6 +1370,10 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
 #ifndef FM_PAIR_HK_WGS
 #define FM_PAIR_HK_WGS 0   // 0: by VPH
 #endif
+// 1: the next unit's loads are issued before the pick (its keys then stay live through it)
+#ifndef FM_PAIR_HK_PF
+#define FM_PAIR_HK_PF 1
+#endif
 constexpr int pair_hk_wgs(int vph) {
     return FM_PAIR_HK_WGS > 0 ? FM_PAIR_HK_WGS : (vph <= 16 ? 12 : (vph <= 24 ? 10 : 8));
 }
@@ -1603,8 +1607,8 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
                 sm.ni[h][2] = chi;
             }
             // xk is dead from here on: the next unit's loads fly during the sorts and gathers
-            if (more) Ln = load(s_nx, c_nx);
-            prefetched = true;
+            if (FM_PAIR_HK_PF && more) Ln = load(s_nx, c_nx);
+            prefetched = FM_PAIR_HK_PF != 0;
             __syncthreads();
             // ---- 4. one tail per wave over both halves' candidates
             const int t = h;

@@ -25,6 +25,9 @@ def main(steps=3):
         E.stream_probe(buf)
     del buf
     panel = E.panel_synthetic(600, 5000, 1, device=dev)
+    if os.environ.get("FM_PLANES") == "1":   # the bench's split panel (fm_split_planes)
+        E.split_planes(panel)
+    panel.chunk_policy = E.chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len)   # as bench.make_step
     cfg = LW.PipelineConfig()
     for _ in range(steps):
         LW.run_pipeline(panel, cfg)
