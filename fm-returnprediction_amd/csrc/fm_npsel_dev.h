@@ -103,7 +103,7 @@ __device__ __forceinline__ void np_swap1(A arr, int i, int j) {   // lane 0
 
 // dumb_select_: selection sort of positions [b, b + kth] over [b, b + num) (first minimum wins)
 template <class A>
-__device__ void np_dumb_select(A arr, int b, int num, int kth) {
+__device__ __forceinline__ void np_dumb_select(A arr, int b, int num, int kth) {
     const int lane = lane_id();
     for (int i = 0; i <= kth; ++i) {
         double mv = 0.0;
@@ -127,7 +127,7 @@ __device__ void np_dumb_select(A arr, int b, int num, int kth) {
 // unguarded_partition_: stoppers found 64 positions at a time (see the header comment).
 // In: ll / hh the scans' starting cursors (exclusive); out: where they stopped.
 template <class A>
-__device__ void np_hoare(A arr, int n, double pv, int& ll, int& hh) {
+__device__ __forceinline__ void np_hoare(A arr, int n, double pv, int& ll, int& hh) {
     const int lane = lane_id();
     // every round swaps >= 1 pair, steps a window past stopper-free positions or ends: the
     // bound only guards against a hang (tests/test_npsel_batch.py checks the loop on the CPU)
@@ -166,8 +166,15 @@ __device__ void np_hoare(A arr, int n, double pv, int& ll, int& hh) {
     }
 }
 
+// D: levels of median-of-medians recursion replayed exactly; past them the inner selection
+// uses median-of-3 pivots (differs from numpy only if the selection over the medians ALSO
+// exhausts its depth limit -- adversarial data at two levels at once).  Everything is inlined:
+// no call stack, no scratch.
+#ifndef FM_NP_MOM_DEPTH
+#define FM_NP_MOM_DEPTH 1
+#endif
 template <int D, class A>
-__device__ void np_introselect(A arr, int num, int kth, int& piv, int& npiv, bool stack);
+__device__ __forceinline__ void np_introselect(A arr, int num, int kth, int& piv, int& npiv, bool stack);
 
 // median5_: index (0..4) of the median of arr[0..5), with numpy's swaps (lane 0)
 template <class A>
@@ -191,7 +198,7 @@ __device__ __forceinline__ int np_median5(A v) {
 // median_of_median5_ on arr[0..num): the groups' medians moved to the front, then the median
 // of those by a stack-less introselect (depth-bounded here: D levels)
 template <int D, class A>
-__device__ int np_mom5(A arr, int num) {
+__device__ __forceinline__ int np_mom5(A arr, int num) {
     const int nmed = num / 5;
     if (lane_id() == 0) {
         for (int i = 0, sl = 0; i < nmed; ++i, sl += 5) {
@@ -213,7 +220,7 @@ __device__ int np_mom5(A arr, int num) {
 
 // introselect_<double_tag, false>: kth of arr[0..num) (stack == false: no pivot stack)
 template <int D, class A>
-__device__ void np_introselect(A arr, int num, int kth, int& piv, int& npiv, bool stack) {
+__device__ __forceinline__ void np_introselect(A arr, int num, int kth, int& piv, int& npiv, bool stack) {
     const int lane = lane_id();
     int low = 0, high = num - 1;
     if (stack) {
@@ -290,17 +297,18 @@ __device__ void np_introselect(A arr, int num, int kth, int& piv, int& npiv, boo
 // arr[i], arr[i+1] after np.percentile's partition of arr[0..n) (i < 0: the rank is past
 // n - 2, numpy's index -1 for both; kth = [0, n-1]).  Wave-uniform results.
 template <class A>
-__device__ void np_percentile_pair(A arr, int n, int i, double& va, double& vb) {
+__device__ __forceinline__ void np_percentile_pair(A arr, int n, int i, double& va, double& vb) {
     // kth = np.unique([0, -1, i, i+1]) made non-negative and sorted: [0, i (i > 0), i+1, n-1]
     // (i+1 == n-1 stays a duplicate: its second introselect finds the pivot and returns);
-    // the rank past n - 2 (i < 0): [0, n-1].  Straight-line: no private arrays.
+    // the rank past n - 2 (i < 0): [0, n-1].  One loop (one inlined copy), no private arrays.
     int piv = 0, npiv = 0;
-    np_introselect<4>(arr, n, 0, piv, npiv, true);
-    if (i >= 0) {
-        if (i > 0) np_introselect<4>(arr, n, i, piv, npiv, true);
-        np_introselect<4>(arr, n, i + 1, piv, npiv, true);
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+        if (i < 0 && (q == 1 || q == 2)) continue;
+        if (q == 1 && i == 0) continue;
+        const int kth = q == 0 ? 0 : (q == 1 ? i : (q == 2 ? i + 1 : n - 1));
+        np_introselect<FM_NP_MOM_DEPTH>(arr, n, kth, piv, npiv, true);
     }
-    np_introselect<4>(arr, n, n - 1, piv, npiv, true);
     arr.sync();
     const int ia = i < 0 ? n - 1 : i, ib = i < 0 ? n - 1 : i + 1;
     va = arr.ld(ia);

@@ -165,7 +165,7 @@ union FixSmem {
 
 // wave 0: the exactly-zero numpy cuts of unit (s, c), written by this workgroup just before
 template <class A>
-__device__ void zero_sign_unit(const SelArgs& a, int s, int c, A arr) {
+__device__ __forceinline__ void zero_sign_unit(const SelArgs& a, int s, int c, A arr) {
     const int lane = lane_id();
     const int64_t o = (int64_t)c * a.nseg + s;
     auto ld = [](const double* p) {
