@@ -179,10 +179,13 @@ __device__ __forceinline__ void zero_sign_unit(const SelArgs& a, int s, int c, A
     const int L = (int)(a.seg_off[s + 1] - r0);
     const double* src = a.cols + (int64_t)c * a.col_stride + r0;
     const uint8_t* msk = a.mask ? a.mask + r0 : nullptr;
-    // the values np.percentile sees: the unit's non-NaN (row-mask selected) rows, frame order
+    // the values np.percentile sees: the unit's non-NaN (row-mask selected) rows, frame order;
+    // also how many are < 0 and == 0 (the zero run's ranks in sorted order)
+    int nneg = 0, nzero = 0;
     auto fill = [&](bool& both) -> int {
         int cnt = 0;
         bool ng = false, ps = false;
+        nneg = nzero = 0;
         for (int b = 0; b < L; b += WAVE) {
             const int r = b + lane;
             double x = r < L ? src[r] : (double)NAN;
@@ -194,25 +197,55 @@ __device__ __forceinline__ void zero_sign_unit(const SelArgs& a, int s, int c, A
             const bool z = x == 0.0;
             ng = ng || (z && __double_as_longlong(x) < 0);
             ps = ps || (z && __double_as_longlong(x) >= 0);
+            nneg += (int)__popcll(__ballot(x < 0.0));
+            nzero += (int)__popcll(__ballot(z));
         }
         arr.sync();
         both = __ballot(ng) != 0ull && __ballot(ps) != 0ull;
         return cnt;
     };
+    // the k-th zero of arr[0..n) in frame order (pandas: lexsort keeps equal values in order)
+    auto kth_zero = [&](int n, int k) -> double {
+        int seen = 0;
+        for (int b = 0; b < n; b += WAVE) {
+            const int r = b + lane;
+            const double x = r < n ? arr.ld(r) : 1.0;
+            const uint64_t zb = __ballot(x == 0.0);
+            const int c = (int)__popcll(zb);
+            if (k < seen + c) {
+                uint64_t m = zb;
+                for (int q = 0; q < k - seen; ++q) m &= m - 1;
+                return __shfl(x, __builtin_ctzll(m), WAVE);
+            }
+            seen += c;
+        }
+        return 0.0;
+    };
     bool both = false;
     int n = fill(both);
-    if (!both) return;   // one kind of zero: the key order already gave numpy's bits
+    if (!both) return;   // one kind of zero: the key order already gave the reference's bits
     for (int t = 0; t < 2; ++t) {
         if (t == 0 ? !zl : !zh) continue;
-        if (t == 1 && zl) n = fill(both);   // each np.percentile call partitions its own copy
         const double q = t == 0 ? a.q_lo : a.q_hi;
         int i, j;
         double g;
-        qranks(n, q, 0, i, j, g);
-        const bool top = (double)(n - 1) * q >= (double)(n - 1);
-        double va, vb;
-        np_percentile_pair(arr, n, top ? -1 : i, va, vb);
-        const double r = qlerp(va, vb, g, 0);
+        qranks(n, q, a.lerp_mode, i, j, g);
+        double r;
+        if (a.lerp_mode == 0) {
+            if (t == 1 && zl) n = fill(both);   // each np.percentile call partitions its own copy
+            const bool top = (double)(n - 1) * q >= (double)(n - 1);
+            double va, vb;
+            np_percentile_pair(arr, n, top ? -1 : i, va, vb);
+            r = qlerp(va, vb, g, 0);
+        } else {
+            // pandas group_quantile: v[i] (+ (v[j] - v[i]) * g); a zero cut with a nonzero
+            // operand keeps the select's value (its sign comes from the arithmetic)
+            const bool za = i >= nneg && i < nneg + nzero, zb = j >= nneg && j < nneg + nzero;
+            if (!(za && (g == 0.0 || zb))) continue;
+            const double va = kth_zero(n, i - nneg);
+            const double vb = g == 0.0 ? va : kth_zero(n, j - nneg);
+            r = qlerp(va, vb, g, 1);
+        }
         if (lane == 0) (t == 0 ? a.lo : a.hi)[o] = r;
     }
 }
@@ -224,6 +257,10 @@ __global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs,
     SelArgs b = a;
     b.ctl = nullptr;
     const uint32_t nw = __hip_atomic_load(&ctl->nwork, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // an empty list (every workgroup reads the same count: nothing appends during this launch)
+    // needs no reset: exit without touching the done counter (256 same-address atomics cost
+    // more than the whole no-op launch)
+    if (nw == 0) return;
     for (uint32_t i = blockIdx.x; i < nw; i += gridDim.x) {
         const uint32_t u = ctl->work[i];
         const int s = (int)(u % (uint32_t)b.nseg), c = (int)(u / (uint32_t)b.nseg);
@@ -231,7 +268,7 @@ __global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs,
         else stream_unit(b, s, c, sm.sel);
         __threadfence();
         __syncthreads();
-        if (b.lerp_mode == 0 && threadIdx.x < WAVE) {
+        if (threadIdx.x < WAVE) {
             const int64_t L = b.seg_off[s + 1] - b.seg_off[s];
             if (L <= ZS_LDS) zero_sign_unit(b, s, c, NpLds{sm.arr});
             else zero_sign_unit(b, s, c, NpGlobal{zs + (int64_t)blockIdx.x * zs_len});
