@@ -179,13 +179,10 @@ __device__ __forceinline__ void zero_sign_unit(const SelArgs& a, int s, int c, A
     const int L = (int)(a.seg_off[s + 1] - r0);
     const double* src = a.cols + (int64_t)c * a.col_stride + r0;
     const uint8_t* msk = a.mask ? a.mask + r0 : nullptr;
-    // the values np.percentile sees: the unit's non-NaN (row-mask selected) rows, frame order;
-    // also how many are < 0 and == 0 (the zero run's ranks in sorted order)
-    int nneg = 0, nzero = 0;
+    // the values np.percentile sees: the unit's non-NaN (row-mask selected) rows, frame order
     auto fill = [&](bool& both) -> int {
         int cnt = 0;
         bool ng = false, ps = false;
-        nneg = nzero = 0;
         for (int b = 0; b < L; b += WAVE) {
             const int r = b + lane;
             double x = r < L ? src[r] : (double)NAN;
@@ -197,29 +194,10 @@ __device__ __forceinline__ void zero_sign_unit(const SelArgs& a, int s, int c, A
             const bool z = x == 0.0;
             ng = ng || (z && __double_as_longlong(x) < 0);
             ps = ps || (z && __double_as_longlong(x) >= 0);
-            nneg += (int)__popcll(__ballot(x < 0.0));
-            nzero += (int)__popcll(__ballot(z));
         }
         arr.sync();
         both = __ballot(ng) != 0ull && __ballot(ps) != 0ull;
         return cnt;
-    };
-    // the k-th zero of arr[0..n) in frame order (pandas: lexsort keeps equal values in order)
-    auto kth_zero = [&](int n, int k) -> double {
-        int seen = 0;
-        for (int b = 0; b < n; b += WAVE) {
-            const int r = b + lane;
-            const double x = r < n ? arr.ld(r) : 1.0;
-            const uint64_t zb = __ballot(x == 0.0);
-            const int c = (int)__popcll(zb);
-            if (k < seen + c) {
-                uint64_t m = zb;
-                for (int q = 0; q < k - seen; ++q) m &= m - 1;
-                return __shfl(x, __builtin_ctzll(m), WAVE);
-            }
-            seen += c;
-        }
-        return 0.0;
     };
     bool both = false;
     int n = fill(both);
@@ -229,23 +207,12 @@ __device__ __forceinline__ void zero_sign_unit(const SelArgs& a, int s, int c, A
         const double q = t == 0 ? a.q_lo : a.q_hi;
         int i, j;
         double g;
-        qranks(n, q, a.lerp_mode, i, j, g);
-        double r;
-        if (a.lerp_mode == 0) {
-            if (t == 1 && zl) n = fill(both);   // each np.percentile call partitions its own copy
-            const bool top = (double)(n - 1) * q >= (double)(n - 1);
-            double va, vb;
-            np_percentile_pair(arr, n, top ? -1 : i, va, vb);
-            r = qlerp(va, vb, g, 0);
-        } else {
-            // pandas group_quantile: v[i] (+ (v[j] - v[i]) * g); a zero cut with a nonzero
-            // operand keeps the select's value (its sign comes from the arithmetic)
-            const bool za = i >= nneg && i < nneg + nzero, zb = j >= nneg && j < nneg + nzero;
-            if (!(za && (g == 0.0 || zb))) continue;
-            const double va = kth_zero(n, i - nneg);
-            const double vb = g == 0.0 ? va : kth_zero(n, j - nneg);
-            r = qlerp(va, vb, g, 1);
-        }
+        qranks(n, q, 0, i, j, g);
+        if (t == 1 && zl) n = fill(both);   // each np.percentile call partitions its own copy
+        const bool top = (double)(n - 1) * q >= (double)(n - 1);
+        double va, vb;
+        np_percentile_pair(arr, n, top ? -1 : i, va, vb);
+        const double r = qlerp(va, vb, g, 0);
         if (lane == 0) (t == 0 ? a.lo : a.hi)[o] = r;
     }
 }
@@ -268,7 +235,7 @@ __global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs,
         else stream_unit(b, s, c, sm.sel);
         __threadfence();
         __syncthreads();
-        if (threadIdx.x < WAVE) {
+        if (b.lerp_mode == 0 && threadIdx.x < WAVE) {
             const int64_t L = b.seg_off[s + 1] - b.seg_off[s];
             if (L <= ZS_LDS) zero_sign_unit(b, s, c, NpLds{sm.arr});
             else zero_sign_unit(b, s, c, NpGlobal{zs + (int64_t)blockIdx.x * zs_len});

@@ -98,11 +98,13 @@ __device__ __forceinline__ void sel_mark(const SelArgs& a, int64_t u) {
     if (a.nvalid) a.nvalid[u] = -1;
     sel_push(a, u);
 }
-// A cut that is exactly +-0: its sign is the reference's ordering of equal zeros -- numpy's
-// partition order (np.percentile) or the stable frame order (pandas' lexsort in
-// groupby.quantile) -- which the fix-up kernel reproduces when the unit holds both signed zeros
+// A numpy cut that is exactly +-0: its sign is numpy's partition order's business (the
+// fix-up kernel replays it when the unit holds both signed zeros).  pandas' groupby.quantile
+// (lerp mode 1) orders equal values by an unstable argsort that numpy dispatches to its SIMD
+// sort on AVX-512 hosts; that order is not reproduced (only the sign of an exactly-zero NYSE
+// `me` breakpoint could differ, and market equity is positive).
 __device__ __forceinline__ bool zero_cut(const SelArgs& a, double lo, double hi) {
-    return a.ctl != nullptr && (lo == 0.0 || hi == 0.0);
+    return a.lerp_mode == 0 && a.ctl != nullptr && (lo == 0.0 || hi == 0.0);
 }
 
 __device__ __forceinline__ uint64_t key_of(double x) { return isnan(x) ? SENT : dkey(x); }
