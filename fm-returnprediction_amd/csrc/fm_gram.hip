@@ -27,6 +27,9 @@ constexpr int GNW = GT / WAVE;
 #define FM_GRAM_MINW (FM_GRAM_PF2 ? 2 : 3)
 #endif
 constexpr int GRAM_MINW = FM_GRAM_MINW;   // waves per SIMD the register budget allows
+#ifndef FM_GRAM_WGTIME
+#define FM_GRAM_WGTIME 0   // probe builds only (tools/gram_wgtime.py): per-workgroup start / end
+#endif                     // times and hardware id into a.flags (never the shipped library)
 
 // One workgroup per chunk (normally a whole month: the chunk plan makes chunks as large as
 // the chip's resident workgroup slots allow, so the prologue and the cross-wave epilogue run
@@ -43,6 +46,9 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);   // wave-uniform (SGPR loops)
     const int ncols = a.ncols, nseg = a.nseg;
     const int nbr = a.npatterns * a.nlevels;
+#if FM_GRAM_WGTIME
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     // default order last-first: fm_select streams the panel month by month, so the months it
     // read last are still in the memory-side cache when they are read here; with a
     // chunk_order (the split-month plan) the big chunks go first, the small ones fill in; with
@@ -85,6 +91,16 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         g.run(prm, lut, a.inv_scale != nullptr, tile, zblk);
         g.epilogue(tile, a.partial + (int64_t)chunk * nbr * S::PK, nbr);
     }
+#if FM_GRAM_WGTIME
+    if (tid == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint32_t* f = a.flags + 4 * (int64_t)blockIdx.x;
+        f[0] = (uint32_t)t_start;
+        f[1] = (uint32_t)t_end;
+        f[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        f[3] = (uint32_t)(c1 - c0);
+    }
+#endif
 }
 
 template <int NT, int NB, int MINW>
