@@ -29,7 +29,11 @@ constexpr int GNW = GT / WAVE;
 constexpr int GRAM_MINW = FM_GRAM_MINW;   // waves per SIMD the register budget allows
 #ifndef FM_GRAM_WGTIME
 #define FM_GRAM_WGTIME 0   // probe builds only (tools/gram_wgtime.py): per-workgroup start / end
-#endif                     // times and hardware id into a.flags (never the shipped library)
+#endif                     // times and hardware id (never the shipped library)
+#if FM_GRAM_WGTIME
+constexpr int WGT_MAX = 1 << 16;
+__device__ uint32_t g_wgtime[4 * WGT_MAX];   // the probe's own buffer, bounds-checked
+#endif
 
 // One workgroup per chunk (normally a whole month: the chunk plan makes chunks as large as
 // the chip's resident workgroup slots allow, so the prologue and the cross-wave epilogue run
@@ -92,9 +96,9 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         g.epilogue(tile, a.partial + (int64_t)chunk * nbr * S::PK, nbr);
     }
 #if FM_GRAM_WGTIME
-    if (tid == 0) {
+    if (tid == 0 && blockIdx.x < WGT_MAX) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        uint32_t* f = a.flags + 4 * (int64_t)blockIdx.x;
+        uint32_t* f = g_wgtime + 4 * (int64_t)blockIdx.x;
         f[0] = (uint32_t)t_start;
         f[1] = (uint32_t)t_end;
         f[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
@@ -114,6 +118,13 @@ void launch_gram(const fm_gram_args& a, hipStream_t st) {
 
 }  // namespace
 }  // namespace fm
+
+#if FM_GRAM_WGTIME
+extern "C" int fm_gram_wgtime_copy(uint32_t* host, int32_t n) {   // probe builds only
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(fm::g_wgtime), (size_t)4 * (n < fm::WGT_MAX ? n : fm::WGT_MAX) * 4) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int fm_gram(const fm_gram_args* args, void* stream) {
     using namespace fm;

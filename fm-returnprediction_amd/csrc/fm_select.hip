@@ -810,28 +810,66 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
         if (ok) {
             // candidates: key <= tl (a prefix of the sorted values) / HK_MAX - key <= tu (a
             // suffix); NaN keys fail both (the subtraction wraps them above every tu)
-            int wl = 0, wh = 0;
-#pragma unroll
-            for (int v = 0; v < VPT; ++v) {
-                uint32_t k = hk[v];
-                asm volatile("" : "+v"(k));   // no values derived in the count loop kept for here
-                wl += (int)__popcll(__ballot(k <= tl));
-                wh += (int)__popcll(__ballot(HK_MAX - k <= tu));
-                asm volatile("" : "+s"(wl), "+s"(wh));   // counts in order (no spilled masks)
-            }
-            if (lane == 0) {
-                sm.wc[0][w] = wl;
-                sm.wc[1][w] = wh;
-            }
-            __syncthreads();
             int ol = 0, oh = LCAP;
+            for (int pass = 0; pass < 2; ++pass) {   // a second pass only after a refinement
+                int wl = 0, wh = 0;
 #pragma unroll
-            for (int q = 0; q < LNW; ++q) {
-                const int a0 = sm.wc[0][q], a1 = sm.wc[1][q];
-                ol += q < w ? a0 : 0;
-                oh += q < w ? a1 : 0;
-                clo += a0;
-                chi += a1;
+                for (int v = 0; v < VPT; ++v) {
+                    uint32_t k = hk[v];
+                    asm volatile("" : "+v"(k));   // no values derived in the count loop kept for here
+                    wl += (int)__popcll(__ballot(k <= tl));
+                    wh += (int)__popcll(__ballot(HK_MAX - k <= tu));
+                    asm volatile("" : "+s"(wl), "+s"(wh));   // counts in order (no spilled masks)
+                }
+                if (lane == 0) {
+                    sm.wc[0][w] = wl;
+                    sm.wc[1][w] = wh;
+                }
+                __syncthreads();
+                ol = 0;
+                oh = LCAP;
+                clo = chi = 0;
+#pragma unroll
+                for (int q = 0; q < LNW; ++q) {
+                    const int a0 = sm.wc[0][q], a1 = sm.wc[1][q];
+                    ol += q < w ? a0 : 0;
+                    oh += q < w ? a1 : 0;
+                    clo += a0;
+                    chi += a1;
+                }
+                if (pass == 1 || !((clo > LCAP || chi > LCAP) && clo > kl && chi > ku)) break;   // block-uniform
+                // more candidates than a list holds (the thread-minimum thresholds can overshoot
+                // by hundreds): the smallest threshold whose VALUE count still reaches the rank,
+                // by bisection on the keys (block counts; a few passes over the registers),
+                // then recount -- instead of sending the unit to the streaming fix-up
+                auto count_le = [&](uint32_t T, bool upper) -> int {
+                    int c = 0;
+#pragma unroll
+                    for (int v = 0; v < VPT; ++v) {
+                        uint32_t k = hk[v];
+                        asm volatile("" : "+v"(k));
+                        c += (int)__popcll(__ballot(upper ? HK_MAX - k <= T : k <= T));
+                        asm volatile("" : "+s"(c));
+                    }
+                    return block_sum<LNW>(lane == 0 ? c : 0, sm.hs.ints);
+                };
+                auto refine = [&](uint32_t& T, int& cnt, int need, bool upper) {
+                    uint32_t lo = 0, hi = T;
+                    while (cnt > LCAP && lo < hi) {   // block-uniform
+                        const uint32_t mid = lo + (hi - lo) / 2;
+                        const int c = count_le(mid, upper);
+                        if (c >= need) {
+                            hi = mid;
+                            cnt = c;
+                        } else {
+                            lo = mid + 1;
+                        }
+                    }
+                    T = hi;
+                };
+                if (clo > LCAP) refine(tl, clo, kl + 1, false);
+                if (chi > LCAP) refine(tu, chi, ku + 1, true);
+                __syncthreads();   // every pass-0 read of sm.wc before the recount rewrites it
             }
             ok = clo <= LCAP && chi <= LCAP && clo + chi <= n && clo > kl && chi > ku;
             if (ok) {

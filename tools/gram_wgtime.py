@@ -24,15 +24,15 @@ def run(panel, pol):
     for _ in range(3):
         LW.run_pipeline(panel, cfg)
     torch.cuda.synchronize()
-    ga = E.LAST_LAUNCH["fm_gram"][1]   # the captured GramArgs
+    ga = E.LAST_LAUNCH["fm_gram"][1]   # the captured GramArgs (the last model group's launch)
     nwg = ga.nwg if ga.wg_chunk_off else ga.nchunks
-    # re-issue the launch with a fresh flags buffer large enough for the probe
-    flags = torch.zeros(4 * nwg + 64, dtype=torch.int32, device=panel.cols.device)
-    ga.flags = flags.data_ptr()
     for _ in range(3):
         E.L.call("fm_gram", E.L.C.byref(ga), E._stream())
     torch.cuda.synchronize()
-    f = flags[: 4 * nwg].view(nwg, 4).cpu().numpy().astype(np.uint32).astype(np.int64)
+    import ctypes
+    host = (ctypes.c_uint32 * (4 * nwg))()
+    assert E.L.load().fm_gram_wgtime_copy(host, nwg) == 0
+    f = np.frombuffer(host, dtype=np.uint32).reshape(nwg, 4).astype(np.int64)
     t0, t1, hw, nch = f[:, 0], f[:, 1], f[:, 2], f[:, 3]
     base = t0.min()
     s, e = (t0 - base) * 10, (t1 - base) * 10   # ns
