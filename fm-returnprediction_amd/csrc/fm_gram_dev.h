@@ -35,6 +35,9 @@
 #ifndef FM_GRAM_PF2
 #define FM_GRAM_PF2 0   // 1: two tiles of row loads in flight per wave (two register buffers)
 #endif
+#ifndef FM_GRAM_TOUCH
+#define FM_GRAM_TOUCH 1   // 1: one 4-byte load per 128-byte line of the tile after next (L2 warm-up)
+#endif
 
 namespace fm {
 namespace {
@@ -120,6 +123,9 @@ struct GramWave {
     double xw[FM_GRAM_PF2 ? ZW - 1 : 1];
     int lw = 0;
     double acc[NB][NI];
+    // touch loads: the previous touch's word (consumed a tile later, when it has landed) and
+    // their xor (kept live so the loads stay; never meaningful)
+    uint32_t tpend = 0, tacc = 0;
 
     __device__ __forceinline__ GramWave(const fm_gram_args& a_, int64_t r0_, int64_t r1_, int w_)
         : a(a_), r0(r0_), r1(r1_), w(w_), lane((int)threadIdx.x & (WAVE - 1)),
@@ -175,7 +181,34 @@ struct GramWave {
         lv = *((gptr)(a.level ? lvbase + tb : lvbase) + (a.level ? lo : 0u));
     }
 
+    // Warm the L2 for tile t: lane l loads one 4-byte word of 128-byte line (l & 3) of column
+    // l >> 2 (FP64 columns: 16 rows a line; planes: 32 rows, lanes 0-1 the high plane, 2-3 the
+    // low one), so ONE load instruction covers the tile's 60 lines; its data is consumed a tile
+    // later.  The wave's own loads of tile t, issued a tile after, then hit the L2 instead of
+    // waiting a loaded-HBM round trip with one tile in flight.
+    __device__ __forceinline__ void touch(int t) {
+        if constexpr (FM_GRAM_TOUCH == 0) return;
+        tacc ^= tpend;
+        if (t >= ntile) return;   // wave-uniform
+        typedef const __attribute__((address_space(1))) uint32_t* gptr32;
+        const int64_t t0 = r0 + (int64_t)t * TR;
+        const int c = lane >> 2, q = lane & 3;
+        const int cc = c < a.ncols ? c : a.ncols - 1;
+        int64_t row = t0 + (PL ? (q & 1) * 32 : q * 16);
+        row = row < r1 - 1 ? row : r1 - 1;
+        const uint32_t* p;
+        if constexpr (PL) p = (q < 2 ? a.hi_plane : a.lo_plane) + (int64_t)cc * a.plane_stride + row;
+        else p = (const uint32_t*)(a.cols + (int64_t)cc * a.col_stride + row);
+        tpend = *(gptr32)p;
+    }
+    __device__ __forceinline__ void touch_sink() {
+        if constexpr (FM_GRAM_TOUCH == 0) return;
+        tacc ^= tpend;
+        if (tacc == 0x9E3779B9u && a.nseg == -7) a.flags[lane] = tacc;   // never true: keeps the loads
+    }
+
     __device__ __forceinline__ void prefetch() {
+        touch(w + NWV);
         if (w < ntile) load_row(w);
         if constexpr (FM_GRAM_PF2 != 0)
             if (w + NWV < ntile) load_row_into(w + NWV, xw, lw);
@@ -266,8 +299,10 @@ struct GramWave {
                         dst[1 + c] = hw_min(hw_max(xv[c], prm[0][c]), prm[1][c]) - prm[2][c];
                 }
             }
-            // this tile's values are consumed: the next tile's loads fly during the MFMAs
+            // this tile's values are consumed: the next tile's loads fly during the MFMAs, and
+            // the one after next is touched into the L2
             if (tnext < ntile) load_row_into(tnext, xv, lv);
+            touch(tnext + NWV);
             // the operand reads below read other lanes' rows of this wave: LDS executes one
             // wave's DS instructions in order, so only compiler reordering must be prevented
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -349,6 +384,7 @@ struct GramWave {
         } else {
             for (int t = w; t < ntile; t += NWV) tile_step(xv, lv, t, t + NWV);
         }
+        touch_sink();
     }
 
     // Cross-wave reduction and store: outp[bucket][packed upper triangle] for the nbr
