@@ -470,6 +470,9 @@ extern "C" int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, in
     FM_REQUIRE(n >= 0, "fm_rolling_std: negative n");
     if (n == 0) return FM_OK;
     FM_REQUIRE(ids && x && out, "fm_rolling_std: null pointer");
+    // the kernel moves row pairs with 16-byte loads / stores from the bases
+    FM_REQUIRE((((uintptr_t)ids | (uintptr_t)x | (uintptr_t)out) & 15) == 0,
+               "fm_rolling_std: ids, x and out must be 16-byte aligned");
     FM_REQUIRE(window >= 1 && window <= 4096, "fm_rolling_std: window must be 1..4096");
     FM_REQUIRE(min_periods >= 1 && min_periods <= window, "fm_rolling_std: min_periods must be 1..window");
     const int E = ST_ROWS + st_halo(window);

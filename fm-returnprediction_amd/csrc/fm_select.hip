@@ -1906,9 +1906,10 @@ extern "C" int64_t fm_select_ws_bytes(int32_t nseg, int32_t ncols, int32_t max_s
 
 namespace fm {
 namespace {
-// fm_select, optionally with get_subsets' NYSE breakpoints + level bytes riding the two-wave
-// kernel's launch (u != NULL); whenever that kernel is not the path taken, the universe is
-// launched by fm_universe after the cuts instead (same outputs).
+// fm_select, optionally with get_subsets' NYSE breakpoints + level bytes (u != NULL): they ride
+// the long-month high-key kernel's launch (6,145 .. 20,480-row months, tail ranks, no row mask:
+// one more grid column); on every other path, including the two-wave and MID kernels, the
+// universe is launched on its own first (fm_universe, or the row-masked select), same outputs.
 int select_impl(const fm_select_args* args, const fm_universe_args* u, void* stream);
 }  // namespace
 }  // namespace fm

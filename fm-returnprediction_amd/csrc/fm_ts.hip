@@ -920,7 +920,9 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
     // (n, Syy and this lane's S column, clamped to a valid row), one round trip instead of one
     // per row
     double scq[NIT][15], n0q[NIT], syq[NIT];
-    if (K < 16) {
+    // (a shard with no months of its own has no moments rows at all: nothing to preload, and
+    // no row below is `mine`)
+    if (K < 16 && a.seg_hi > a.seg_lo) {
         const int bc = b <= K ? b : 0;
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {

@@ -268,8 +268,9 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
     also the clipped mean / sd; ``center``: also a Gram pivot inside the data; ``level``
     (uint8 [rows], one column): every row's (x >= lo) + (x >= hi) (fm_select).
     ``universe`` = (q_a, q_b): also get_subsets' NYSE breakpoints and level bytes of the
-    panel's me / nyse rows in the same call (fm_select_universe: one launch on the two-wave
-    path); returns (Cuts, (cut_a, cut_b, level)) then."""
+    panel's me / nyse rows in the same call (fm_select_universe: riding the long-month
+    kernel's launch for 6,145-20,480-row months without the histogram (MID) variant, its own
+    launch otherwise); returns (Cuts, (cut_a, cut_b, level)) then."""
     src = panel.cols if cols is None else cols
     if src.dim() == 1:
         src = src.view(1, -1)
@@ -1042,10 +1043,15 @@ def rolling_std(ids, x, window=252, min_periods=100, scale=252 ** 0.5, out=None)
     if x.dtype != torch.float64 or x.dim() != 1 or ids.shape[0] != n or x.device != ids.device:
         raise ValueError("rolling_std: x must be a float64 [n] tensor beside int64 [n] ids")
     x = x.contiguous()
+    # fm_rolling_std moves row pairs with 16-byte accesses: views at odd offsets are copied
+    if x.data_ptr() % 16:
+        x = x.clone()
+    if ids.data_ptr() % 16 or not ids.is_contiguous():
+        ids = ids.clone()
     if out is None:
         out = torch.empty(n, dtype=torch.float64, device=x.device)
-    if out.dtype != torch.float64 or out.shape != (n,) or not out.is_contiguous():
-        raise ValueError("rolling_std: out must be a contiguous float64 [n] tensor")
+    if out.dtype != torch.float64 or out.shape != (n,) or not out.is_contiguous() or out.data_ptr() % 16:
+        raise ValueError("rolling_std: out must be a contiguous, 16-byte aligned float64 [n] tensor")
     args = (ids.data_ptr(), x.data_ptr(), n, int(window), int(min_periods), float(scale), out.data_ptr())
     _kcall("fm_rolling_std", "fm_rolling_std", *args, _stream())
     LAST_LAUNCH["fm_rolling_std"] = ("fm_rolling_std", None, ((ids, x, out), args))

@@ -92,7 +92,10 @@ class ShardedStep:
         """Capture the phases as HIP graphs.  Every host-side cache (chunk plans, model
         plans) and the static exchange buffers must exist before capture: without a prior
         eager() step, one is run here first."""
-        if self.exchange and self.rec_g is None:
+        warmed = getattr(self.panel, "_chunk_cache", None) is not None and \
+            bool(getattr(self.panel, "_group_cache", None))
+        if not warmed or (self.exchange and self.rec_g is None):
+            # host-side plans upload with host-to-device copies, which must not be captured
             self.eager()
             torch.cuda.synchronize()
         if not self.exchange:

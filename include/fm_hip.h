@@ -414,7 +414,8 @@ int fm_firm_chars(const fm_chars_args* args, void* stream);
 /* Per-row rolling std (ddof=1) over the last `window` rows of each firm group (rows grouped
  * as for fm_firm_chars), NaN below `min_periods` observations, exactly 0 when all
  * observations are equal, times `scale`.  1 <= window <= 4096, 1 <= min_periods <= window
- * (a std needs at least 2 observations, so min_periods 1 behaves as 2). */
+ * (a std needs at least 2 observations, so min_periods 1 behaves as 2).  ids, x and out must be
+ * 16-byte aligned (row pairs move as 16-byte accesses); FM_EINVAL otherwise. */
 int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, int32_t window,
                    int32_t min_periods, double scale, double* out, void* stream);
 

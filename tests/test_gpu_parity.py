@@ -475,10 +475,10 @@ def test_universe_kernel_vs_oracle(E):
 @pytest.mark.parametrize("maxlen", [6144, 9000, 20000, 24000])
 def test_select_universe_fused(E, maxlen):
     """fm_select_universe: the winsorize cuts and get_subsets' NYSE breakpoints + level bytes
-    from one call.  Months <= 6,144 rows ride the two-wave kernel's launch (the universe
-    months streamed by its workgroups beside the winsorize units), months <= 20,480 rows the
-    long-month kernel's (one more grid column); longer ones take the streaming select and the
-    row-masked NYSE select.  Cuts must equal fm_select's alone bit for bit, breakpoints the
+    from one call.  Months of 6,145-20,480 rows ride the long-month high-key kernel's launch
+    (one more grid column); shorter months (the two-wave kernel) and longer ones (the
+    streaming select) launch the universe on its own first (fm_universe / the row-masked NYSE
+    select).  Cuts must equal fm_select's alone bit for bit, breakpoints the
     pandas lerp restatement and levels the reference's masks, over adversarial me months
     (clusters, ties, NaN me, no NYSE row, every NYSE me NaN, 1-row months)."""
     rng = np.random.default_rng(77)
