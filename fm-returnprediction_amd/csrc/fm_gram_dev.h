@@ -36,7 +36,8 @@
 #define FM_GRAM_PF2 0   // 1: two tiles of row loads in flight per wave (two register buffers)
 #endif
 #ifndef FM_GRAM_TOUCH
-#define FM_GRAM_TOUCH 1   // 1: one 4-byte load per 128-byte line of the tile after next (L2 warm-up)
+#define FM_GRAM_TOUCH 0   // 1: one 4-byte load per 128-byte line of the tile after next (L2 warm-up;
+                          // measured 123.4 vs 110.3 us without: not used)
 #endif
 
 namespace fm {
