@@ -24,7 +24,8 @@ def main(steps=3):
     for _ in range(3):
         E.stream_probe(buf)
     del buf
-    panel = E.panel_synthetic(600, 5000, 1, device=dev)
+    T, N = (1000, 20000) if os.environ.get("FM_PMC_LONG") == "1" else (600, 5000)   # C5-shaped months
+    panel = E.panel_synthetic(T, N, 1, device=dev)
     if os.environ.get("FM_PLANES") == "1":   # the bench's split panel (fm_split_planes)
         E.split_planes(panel)
     panel.chunk_policy = E.chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len)   # as bench.make_step
