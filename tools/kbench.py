@@ -20,6 +20,10 @@ def child():
     panel = E.panel_synthetic(600, 5000, 1, device=dev)
     if os.environ.get("KB_CHUNK"):   # Gram chunk-size A/B (rows per workgroup)
         panel.chunk_rows = int(os.environ["KB_CHUNK"])
+    if os.environ.get("KB_POLICY") == "months":   # whole-month Gram chunks instead of the default plan
+        panel.chunk_policy = ("months", panel.max_seg_len)
+    if os.environ.get("KB_PLANES") == "1":   # the split panel (fm_split_planes)
+        E.split_planes(panel)
     cfg = LW.PipelineConfig()
     for _ in range(3):
         LW.run_pipeline(panel, cfg)
@@ -44,6 +48,7 @@ def main():
             continue
         d = json.loads(line[0][3:])
         tag = os.path.basename(os.path.dirname(lib)) + (f"[chunk {os.environ['KB_CHUNK']}]" if os.environ.get("KB_CHUNK") else "")
+        tag += "".join(f"[{k}={os.environ[k]}]" for k in ("KB_POLICY", "KB_PLANES") if os.environ.get(k))
         print(tag, " ".join(f"{k}={v * 1e3:.1f}us" for k, v in d.items()), flush=True)
 
 
