@@ -30,6 +30,45 @@ int check_launch(const char* what);
 constexpr uint64_t SENT = ~0ull;   // key of NaN / absent values: sorts after +inf
 constexpr int WAVE = 64;
 
+// Phase probe (timing builds only, tools/build_variant.sh probe "-DFM_PROBE=1" ...;
+// tools/tail_probe.py): thread 0 of a workgroup writes s_memrealtime (100 MHz) at numbered
+// points of a kernel into that translation unit's own bounded buffer (FM_PROBE_BUFFER), read
+// back by fm_probe_copy_<tu>.  Compiled out of the shipped library.
+#ifndef FM_PROBE
+#define FM_PROBE 0
+#endif
+constexpr int PROBE_WG = 8192, PROBE_SLOTS = 8;
+#if FM_PROBE
+#define FM_PROBE_BUFFER(tu)                                                                  \
+    namespace fm {                                                                           \
+    __device__ uint32_t g_probe_##tu[PROBE_SLOTS * PROBE_WG];                                \
+    }                                                                                        \
+    extern "C" int fm_probe_copy_##tu(uint32_t* host, int32_t nwg) {                         \
+        const int n = nwg < ::fm::PROBE_WG ? nwg : ::fm::PROBE_WG;                           \
+        return hipMemcpyFromSymbol(host, HIP_SYMBOL(::fm::g_probe_##tu),                     \
+                                   (size_t)n * ::fm::PROBE_SLOTS * 4) == hipSuccess ? 0 : -1; \
+    }                                                                                        \
+    extern "C" int fm_probe_clear_##tu() {                                                   \
+        void* p_ = nullptr;                                                                  \
+        if (hipGetSymbolAddress(&p_, HIP_SYMBOL(::fm::g_probe_##tu)) != hipSuccess) return -1; \
+        return hipMemset(p_, 0, sizeof(::fm::g_probe_##tu)) == hipSuccess ? 0 : -1;          \
+    }
+#define FM_PROBE_AT(tu, slot)                                                                \
+    do {                                                                                     \
+        if (threadIdx.x == 0) {                                                              \
+            const int64_t w_ = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z); \
+            if (w_ < ::fm::PROBE_WG)                                                         \
+                ::fm::g_probe_##tu[w_ * ::fm::PROBE_SLOTS + (slot)] =                        \
+                    (uint32_t)__builtin_amdgcn_s_memrealtime();                              \
+        }                                                                                    \
+    } while (0)
+#else
+#define FM_PROBE_BUFFER(tu)
+#define FM_PROBE_AT(tu, slot) \
+    do {                      \
+    } while (0)
+#endif
+
 // Order-preserving map double -> uint64 (total order with -0.0 < +0.0; callers map NaN
 // to SENT before calling).
 __device__ __forceinline__ uint64_t dkey(double v) {
@@ -101,6 +140,71 @@ __device__ __forceinline__ uint64_t xor_lanes_u64(uint64_t x, int j) {
 __device__ __forceinline__ double xor_lanes_f64(double x, int j) {
     return __longlong_as_double((long long)xor_lanes_u64((uint64_t)__double_as_longlong(x), j));
 }
+// Any 4- or 8-byte value of lane (this lane ^ J): xor_lanes per 32-bit half (bit-exact
+// __shfl_xor, which is a ds_bpermute -- an LDS round trip per step)
+template <int J, typename T>
+__device__ __forceinline__ T xor_lane(T v) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "xor_lane: 4- or 8-byte values");
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, xor_lanes<J>(__builtin_bit_cast(uint32_t, v)));
+    } else {
+        const uint64_t b = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = xor_lanes<J>((uint32_t)b), hi = xor_lanes<J>((uint32_t)(b >> 32));
+        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+    }
+}
+// Butterfly over the wave (distances 32, 16, .., 1: the order the __shfl_xor loops used, so
+// floating-point sums keep their bits) or over each 16-lane row (8, 4, 2, 1).
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op) {
+    v = op(v, xor_lane<32>(v));
+    v = op(v, xor_lane<16>(v));
+    v = op(v, xor_lane<8>(v));
+    v = op(v, xor_lane<4>(v));
+    v = op(v, xor_lane<2>(v));
+    v = op(v, xor_lane<1>(v));
+    return v;
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T row16_reduce(T v, Op op) {
+    v = op(v, xor_lane<8>(v));
+    v = op(v, xor_lane<4>(v));
+    v = op(v, xor_lane<2>(v));
+    v = op(v, xor_lane<1>(v));
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T row16_sum(T v) {
+    return row16_reduce(v, [](T a, T b) { return a + b; });
+}
+// Value of lane (this lane - O) within this lane's 16-lane row (DPP row_shr; lanes below O
+// in their row get `v` back, like __shfl_up with width 16)
+template <int O, typename T>
+__device__ __forceinline__ T row_shr(T v) {
+    static_assert(O >= 1 && O <= 15, "row_shr: 1..15");
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "row_shr: 4- or 8-byte values");
+    if constexpr (sizeof(T) == 4) {
+        const int x = __builtin_bit_cast(int, v);
+        return __builtin_bit_cast(T, __builtin_amdgcn_update_dpp(x, x, 0x110 + O, 0xF, 0xF, false));
+    } else {
+        const uint64_t b = __builtin_bit_cast(uint64_t, v);
+        const int lo = (int)(uint32_t)b, hi = (int)(uint32_t)(b >> 32);
+        const uint32_t rl = (uint32_t)__builtin_amdgcn_update_dpp(lo, lo, 0x110 + O, 0xF, 0xF, false);
+        const uint32_t rh = (uint32_t)__builtin_amdgcn_update_dpp(hi, hi, 0x110 + O, 0xF, 0xF, false);
+        return __builtin_bit_cast(T, ((uint64_t)rh << 32) | rl);
+    }
+}
+// Inclusive prefix sum of an int over the wave: four DPP row shifts, then row 15 / row 31
+// broadcasts into the later rows (integer adds: the same result as the __shfl_up ladder)
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
 
 // Hardware v_max_f64 / v_min_f64 (IEEE mode: a quiet-NaN operand yields the other one).
 // Inline asm, because the maxnum/minnum lowering canonicalizes its inputs first: an extra
@@ -139,6 +243,13 @@ struct CSum {
     __device__ __forceinline__ void reset() { s = c = 0.0; }
 };
 
+// LDS writes of this wave visible to its other lanes (a wave-local barrier)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 // number of set bits of `mask` strictly below this lane
 __device__ __forceinline__ int mask_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -147,30 +258,16 @@ __device__ __forceinline__ int mask_rank(uint64_t mask) {
 
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-    return v;
+    return wave_reduce(v, [](T a, T b) { return a + b; });
 }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t w = (uint64_t)__shfl_xor((long long)v, o, WAVE);
-        v = w < v ? w : v;
-    }
-    return v;
+    return wave_reduce(v, [](uint64_t a, uint64_t b) { return b < a ? b : a; });
 }
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t w = (uint64_t)__shfl_xor((long long)v, o, WAVE);
-        v = w > v ? w : v;
-    }
-    return v;
+    return wave_reduce(v, [](uint64_t a, uint64_t b) { return b > a ? b : a; });
 }
 __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, WAVE);
-    return v;
+    return wave_reduce(v, [](uint32_t a, uint32_t b) { return a | b; });
 }
 
 // Block-wide reductions for blocks of NW waves; `scratch` holds NW elements.  Every
@@ -214,8 +311,7 @@ __device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t* scratch)
 
 template <int NW>
 __device__ __forceinline__ double block_min_f64(double v, double* scratch) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
+    v = wave_reduce(v, [](double a, double b) { return fmin(a, b); });
     const int w = threadIdx.x / WAVE;
     __syncthreads();
     if (lane_id() == 0) scratch[w] = v;
@@ -252,12 +348,7 @@ template <int NW>
 __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) {
     const int lane = lane_id();
     const int w = threadIdx.x / WAVE;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        int y = __shfl_up(x, o, WAVE);
-        if (lane >= o) x += y;
-    }
+    const int x = wave_incl_scan(v);
     __syncthreads();
     if (lane == WAVE - 1) scratch[w] = x;
     __syncthreads();

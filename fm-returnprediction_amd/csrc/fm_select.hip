@@ -20,6 +20,8 @@
 #include "fm_common.h"
 
 #include "fm_select_dev.h"
+
+FM_PROBE_BUFFER(sel)
 #include "fm_npsel_dev.h"
 
 #ifndef FM_SELECT_STREAM_VPT
@@ -223,10 +225,12 @@ __global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs,
     SelCtl* ctl = a.ctl;
     SelArgs b = a;
     b.ctl = nullptr;
+    FM_PROBE_AT(sel, 4);
     const uint32_t nw = __hip_atomic_load(&ctl->nwork, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // an empty list (every workgroup reads the same count: nothing appends during this launch)
     // needs no reset: exit without touching the done counter (256 same-address atomics cost
     // more than the whole no-op launch)
+    FM_PROBE_AT(sel, 5);
     if (nw == 0) return;
     for (uint32_t i = blockIdx.x; i < nw; i += gridDim.x) {
         const uint32_t u = ctl->work[i];
@@ -1810,6 +1814,7 @@ __global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const d
                                                       uint8_t* __restrict__ level) {
     static_assert(VPT <= 64, "universe_kernel: NYSE flags are one 64-bit mask per thread");
     __shared__ SelSmem sm;
+    FM_PROBE_AT(sel, 0);
     const int s = blockIdx.x, tid = threadIdx.x;
     const int64_t r0 = seg_off[s];
     const int L = (int)(seg_off[s + 1] - r0);
@@ -1849,6 +1854,7 @@ __global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const d
     kmn = block_min_u64<SNW>(kmn, sm.u64s);
     kmx = block_max_u64<SNW>(kmx, sm.u64s + SNW);
     double a = NAN, b = NAN;
+    FM_PROBE_AT(sel, 1);
     if (n > 0) {   // block-uniform
         int rk[4];
         double g0, g1;
@@ -1859,6 +1865,7 @@ __global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const d
         a = qlerp(kval(ko[0]), kval(ko[1]), g0, 1);
         b = qlerp(kval(ko[2]), kval(ko[3]), g1, 1);
     }
+    FM_PROBE_AT(sel, 2);
     if (tid == 0) {
         cut_a[s] = a;
         cut_b[s] = b;
@@ -1868,6 +1875,7 @@ __global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const d
         const int idx = tid + v * ST;
         if (idx < L) level[r0 + idx] = (uint8_t)((xm[v] >= a ? 1 : 0) + (xm[v] >= b ? 1 : 0));
     }
+    FM_PROBE_AT(sel, 3);
 }
 
 }  // namespace

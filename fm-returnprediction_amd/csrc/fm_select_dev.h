@@ -133,12 +133,7 @@ __device__ __forceinline__ uint64_t radix_rank(const double (&xv)[VPT], int rank
             const int h0 = sm.hist[4 * l], h1 = sm.hist[4 * l + 1], h2 = sm.hist[4 * l + 2],
                       h3 = sm.hist[4 * l + 3];
             const int s = h0 + h1 + h2 + h3;
-            int incl = s;
-#pragma unroll
-            for (int o = 1; o < WAVE; o <<= 1) {
-                int y = __shfl_up(incl, o, WAVE);
-                if (l >= o) incl += y;
-            }
+            const int incl = wave_incl_scan(s);
             const int excl = incl - s;
             if (excl <= rem && rem < incl) {
                 int c = excl, b = 4 * l;

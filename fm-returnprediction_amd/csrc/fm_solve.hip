@@ -20,6 +20,8 @@
 
 #include "fm_common.h"
 
+FM_PROBE_BUFFER(solve)
+
 namespace fm {
 namespace {
 
@@ -43,12 +45,6 @@ constexpr double REFIT_REL = 1e-6;
 #ifndef FM_AB_SOLVE_NOMOM
 #define FM_AB_SOLVE_NOMOM 0   // timing builds only (tools/build_variant.sh): skip the moments store
 #endif
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
 
 template <int MD>
 struct WaveScratch {
@@ -389,13 +385,20 @@ __device__ __forceinline__ double rowbc(double v) {
     const uint32_t lo = (uint32_t)rowbc_i<L>((int)(uint32_t)b), hi = (uint32_t)rowbc_i<L>((int)(uint32_t)(b >> 32));
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-__device__ __forceinline__ double rowsum(double v) {
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
-    return v;
-}
+__device__ __forceinline__ double rowsum(double v) { return row16_sum(v); }
 
 constexpr int G16 = 16;   // lanes per problem
+
+template <int NC, int NT>
+union FixSmem;
+inline __device__ bool fix_wanted(uint32_t st, int check_const);
+template <int NC, int NT>
+__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, const double* cols, int64_t stride,
+                        const int64_t* seg_off, int nseg, const double* lo, const double* hi,
+                        const double* shift, const double* inv_scale, const double* add_back,
+                        const uint8_t* level, int nprob, const int32_t* prob_level, const int32_t* prob_z,
+                        const int32_t* prob_nz, const double* moments, int mom_stride, int pmax, double* rec,
+                        uint32_t* status, int check_const);
 
 // 192 threads (three waves, twelve problems at a time: a Table-2 month's 11 problems in ONE
 // round, so no wave factors twice) at two waves per SIMD: 256 VGPRs (the factorization's
@@ -421,6 +424,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     // memory round trip inside the problem loop)
     __shared__ int t_model[S16_MAXP], t_level[S16_MAXP], t_nz[S16_MAXP], t_flags[S16_MAXP];
     __shared__ int t_slot[S16_MAXP];   // wave slot -> problem, by descending K
+    __shared__ uint32_t t_st[S16_MAXP];   // the month's solve status (inline fix-ups)
     __shared__ uint8_t t_z[S16_MAXP][32];
     __shared__ uint32_t t_pat[64];
     __shared__ double t_ab[32];
@@ -446,9 +450,11 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         const int c = tid - 64;   // panel columns past ncols are never indexed
         t_ab[c] = c < a.ab_ncols ? a.add_back[(int64_t)c * a.nseg + s] : 0.0;
     }
+    FM_PROBE_AT(solve, 0);
     const int c0 = a.seg_chunk_off[s], c1 = a.seg_chunk_off[s + 1];
     sum_partials<S16T>(a.partial, c0, c1, nb * zz, bs);
     __syncthreads();
+    FM_PROBE_AT(solve, 1);
     for (int e = tid; e < npat * zz; e += S16T) {   // level-cumulative buckets
         const int pid = e / zz, f = e - pid * zz;
         double* b0 = bs + (int64_t)pid * nl * zz + f;
@@ -459,6 +465,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         }
     }
     __syncthreads();
+    FM_PROBE_AT(solve, 2);
     if (FM_AB_SOLVE_STOP == 1) {
         if (tid == 0) a.status[(int64_t)s * a.nprob] = (uint32_t)bs[0];
         return;
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         const bool skip = !(n >= (double)(K + 1));
         if (live && skip) {
             for (int k = i; k < rs; k += G16) a.rec[ro + k] = k == a.pmax + 1 ? n : NAN;
-            if (i == 0) a.status[(int64_t)s * a.nprob + pp] = FM_ST_SKIPPED;
+            if (i == 0) a.status[(int64_t)s * a.nprob + pp] = t_st[pp] = FM_ST_SKIPPED;
         }
         const bool act0 = live && !skip;
         if (act0 && a.moments && !FM_AB_SOLVE_NOMOM) {
@@ -674,13 +681,29 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                 else if (k == a.pmax + 1) v = n;
                 a.rec[ro + k] = v;
             }
-            if (i == 0) a.status[(int64_t)s * a.nprob + pp] = st | FM_ST_FITTED;
+            if (i == 0) a.status[(int64_t)s * a.nprob + pp] = t_st[pp] = st | FM_ST_FITTED;
+        }
+    }
+    FM_PROBE_AT(solve, 3);
+    // the statsmodels fix-ups of this month's flagged problems (fm_solve_fixup's work, rare),
+    // by this workgroup: its own rec / moments / status writes are visible after the barrier
+    if (a.fix_cols != nullptr) {   // block-uniform
+        __syncthreads();
+        const int ckc = a.fix_check_const;
+        for (int q = 0; q < a.nprob; ++q) {
+            const uint32_t st = t_st[q];
+            if (!fix_wanted(st, ckc)) continue;   // block-uniform
+            fix_one<G16, S16T>(s, q, st, *reinterpret_cast<FixSmem<G16, S16T>*>(&wsc[0][0]), a.fix_cols,
+                               a.fix_stride, a.fix_seg_off, a.nseg, a.fix_lo, a.fix_hi, a.fix_shift,
+                               a.fix_inv_scale, a.add_back, a.fix_level, a.nprob, a.prob_level, a.prob_z,
+                               a.prob_nz, a.moments, a.mom_stride, a.pmax, a.rec, a.status, ckc);
         }
     }
 }
 
 // Exact nonzero-constant test for problems flagged CONST_SUSPECT (statsmodels
 // add_constant(has_constant='skip'): np.ptp(x)==0 & all(x != 0), src/regressions.py:50).
+template <int NT = VT>
 __device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, const double* cols, int64_t stride,
                                            const int64_t* seg_off, int nseg, const double* lo,
                                            const double* hi, const uint8_t* level, int nprob,
@@ -694,7 +717,7 @@ __device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, const do
         const int cx = zi[1 + j] - 1;
         uint64_t kmin = SENT, kmax = 0;
         bool allnz = true;
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += VT) {
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += NT) {
             if (level && (int)level[r] < u) continue;
             bool ok = true;
             double xv = 0.0;
@@ -715,9 +738,9 @@ __device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, const do
             kmax = k > kmax ? k : kmax;
             if (xv == 0.0) allnz = false;
         }
-        kmin = block_min_u64<VNW>(kmin, red);
-        kmax = block_max_u64<VNW>(kmax, red);
-        const int nzr = block_sum<VNW>(allnz ? 0 : 1, (int*)red);
+        kmin = block_min_u64<NT / WAVE>(kmin, red);
+        kmax = block_max_u64<NT / WAVE>(kmax, red);
+        const int nzr = block_sum<NT / WAVE>(allnz ? 0 : 1, (int*)red);
         if (kmin != SENT && kmin == kmax && nzr == 0) any_const = true;
     }
     if (threadIdx.x == 0 && any_const) status[(int64_t)s * nprob + p] |= FM_ST_CONST_COL;
@@ -761,6 +784,7 @@ struct InfySmem {
     int okf;
 };
 
+template <int NT = VT>
 __device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, const double* cols, int64_t stride,
                                           const int64_t* seg_off, int nseg, const double* lo,
                                           const double* hi, const double* shift,
@@ -778,7 +802,7 @@ __device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, const doub
     const int* zi = prob_z + p * 32;
     const double* mo = moments + ((int64_t)s * nprob + p) * mom_stride;
     const double n = mo[0];
-    for (int e = threadIdx.x; e < K * K; e += VT) Lm[(e / K) * 32 + e % K] = mo[1 + K1 + (e / K) * K1 + e % K];
+    for (int e = threadIdx.x; e < K * K; e += NT) Lm[(e / K) * 32 + e % K] = mo[1 + K1 + (e / K) * K1 + e % K];
     if (threadIdx.x < K1) mu[threadIdx.x] = mo[1 + threadIdx.x];
     if (threadIdx.x < 32) bits[threadIdx.x] = 0u;
     __syncthreads();
@@ -805,7 +829,7 @@ __device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, const doub
     __syncthreads();
     if (!okf) return;   // rank-deficient with an inf y: left as computed (NaN)
     const int64_t r0 = seg_off[s], r1 = seg_off[s + 1];
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += VT) {
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += NT) {
         if (level && (int)level[r] < u) continue;
         double v[32];
         bool valid = true;
@@ -890,9 +914,9 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
     return v;
 }
 
-template <int NC>
+template <int NC, int NW = VNW>
 struct RefitSmem {
-    double R[VNW][NC][NC + 1];   // per-wave triangular factors of [1, x, y]
+    double R[NW][NC][NC + 1];    // per-wave triangular factors of [1, x, y]
     double Ac[NC][NC + 1];       // Jacobi: rotated columns of R_xx, Ac[j][i] = (R_xx V)[i][j]
     double Vc[NC][NC + 1];       // Jacobi: V[i][j] at Vc[j][i]
     double bv[NC];
@@ -946,8 +970,8 @@ __device__ __forceinline__ void hh_absorb(double (&a)[NC], double (*R)[NC + 1], 
     });
 }
 
-template <int NC>
-__device__ void refit_pair(int s, int p, RefitSmem<NC>& sm, const double* cols, int64_t stride,
+template <int NC, int NT = VT>
+__device__ void refit_pair(int s, int p, RefitSmem<NC, NT / WAVE>& sm, const double* cols, int64_t stride,
                            const int64_t* seg_off, int nseg, const double* lo, const double* hi,
                            const double* shift, const double* inv_scale, const double* add_back,
                            const uint8_t* level, int nprob, const int32_t* prob_level,
@@ -956,7 +980,8 @@ __device__ void refit_pair(int s, int p, RefitSmem<NC>& sm, const double* cols, 
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
     const int nz = prob_nz[p], P = nz - 1, u = prob_level[p];
     const int* zi = prob_z + p * 32;
-    for (int e = tid; e < VNW * NC * (NC + 1); e += VT) (&sm.R[0][0][0])[e] = 0.0;
+    constexpr int NW = NT / WAVE;
+    for (int e = tid; e < NW * NC * (NC + 1); e += NT) (&sm.R[0][0][0])[e] = 0.0;
     __syncthreads();
     int zc[NC];   // panel column of z index q (q >= 1)
     static_for<0, NC>([&](auto qc) {
@@ -964,7 +989,7 @@ __device__ void refit_pair(int s, int p, RefitSmem<NC>& sm, const double* cols, 
         zc[q] = (q >= 1 && q < nz) ? zi[q] - 1 : 0;
     });
     const int64_t r0 = seg_off[s], r1 = seg_off[s + 1];
-    for (int64_t base = r0 + (int64_t)w * WAVE; base < r1; base += VT) {
+    for (int64_t base = r0 + (int64_t)w * WAVE; base < r1; base += NT) {
         const int64_t r = base + lane;
         bool valid = r < r1 && !(level && (int)level[r] < u);
         double a[NC];
@@ -1000,7 +1025,7 @@ __device__ void refit_pair(int s, int p, RefitSmem<NC>& sm, const double* cols, 
     }
     __syncthreads();
     if (w == 0) {   // merge the other waves' factors into wave 0's
-        for (int o = 1; o < VNW; ++o) {
+        for (int o = 1; o < NW; ++o) {
             double a[NC];
             static_for<0, NC>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
@@ -1090,6 +1115,46 @@ __device__ void refit_pair(int s, int p, RefitSmem<NC>& sm, const double* cols, 
 // statsmodels fix-ups after fm_solve, one workgroup per flagged (month, problem):
 // CONST_SUSPECT (with check_const) -> const_pair; FITTED|INF_IN_Y -> infy_pair;
 // FITTED|REFIT (no inf) -> refit_pair.
+template <int NC, int NT>
+union FixSmem {
+    InfySmem infy;
+    RefitSmem<NC, NT / WAVE> refit;
+    uint64_t red[NT / WAVE];
+};
+static_assert(sizeof(FixSmem<G16, S16T>) <= sizeof(double) * S16W * 4 * G16 * (G16 + 1),
+              "solve16's inline fix-ups reuse its per-wave scratch");
+inline __device__ bool fix_wanted(uint32_t st, int check_const) {
+    return (check_const && (st & FM_ST_CONST_SUSPECT)) ||
+           ((st & FM_ST_FITTED) && (st & (FM_ST_INF_IN_Y | FM_ST_REFIT)));
+}
+// The fix-ups of one flagged (month, problem) whose solve status is `st`, by the whole
+// NT-thread workgroup (block-uniform; ends with the workgroup synchronized)
+template <int NC, int NT>
+__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, const double* cols,
+                                        int64_t stride, const int64_t* seg_off, int nseg, const double* lo,
+                                        const double* hi, const double* shift, const double* inv_scale,
+                                        const double* add_back, const uint8_t* level, int nprob,
+                                        const int32_t* prob_level, const int32_t* prob_z,
+                                        const int32_t* prob_nz, const double* moments, int mom_stride,
+                                        int pmax, double* rec, uint32_t* status, int check_const) {
+    if (check_const && (st & FM_ST_CONST_SUSPECT)) {
+        const_pair<NT>(s, p, sm.red, cols, stride, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
+                       prob_nz, status);
+        __syncthreads();
+    }
+    if (!(st & FM_ST_FITTED)) return;
+    if (st & FM_ST_INF_IN_Y) {
+        infy_pair<NT>(s, p, sm.infy, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level,
+                      nprob, prob_level, prob_z, prob_nz, moments, mom_stride, pmax, rec);
+    } else if ((st & FM_ST_REFIT) && !(st & FM_ST_INF_IN_X) && prob_nz[p] <= NC) {
+        refit_pair<NC, NT>(s, p, sm.refit, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back,
+                           level, nprob, prob_level, prob_z, prob_nz, pmax, rec, status);
+    } else {
+        return;
+    }
+    __syncthreads();   // sm is reused by the next pair
+}
+
 template <int NC>
 __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t stride,
                                                    const int64_t* seg_off, int nseg, const double* lo,
@@ -1101,11 +1166,7 @@ __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t s
                                                    int npairs, const double* moments, int mom_stride,
                                                    int pmax, double* rec, uint32_t* status,
                                                    int check_const) {
-    __shared__ union U {
-        InfySmem infy;
-        RefitSmem<NC> refit;
-        uint64_t red[VNW];
-    } sm;
+    __shared__ FixSmem<NC, VT> sm;
     // npairs < 0: scan every (month, problem) for the flags (no host round trip).  Each
     // workgroup reads VT status words at once and lists the flagged pairs in LDS (a
     // pair-by-pair scan would wait out one memory round trip per pair), then fixes them.
@@ -1113,6 +1174,7 @@ __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t s
     __shared__ int nflag;
     const int total = npairs < 0 ? nseg * nprob : npairs;
     const int tid = threadIdx.x;
+    FM_PROBE_AT(solve, 4);
     for (int base = blockIdx.x * VT; base < total; base += gridDim.x * VT) {
         if (tid == 0) nflag = 0;
         __syncthreads();
@@ -1127,10 +1189,8 @@ __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t s
                     s = pairs[2 * e];
                     p = pairs[2 * e + 1];
                 }
-                const uint32_t st = status[(int64_t)s * nprob + p];
-                const bool want = (check_const && (st & FM_ST_CONST_SUSPECT)) ||
-                                  ((st & FM_ST_FITTED) && (st & (FM_ST_INF_IN_Y | FM_ST_REFIT)));
-                if (want) flagged[atomicAdd(&nflag, 1)] = s * nprob + p;
+                if (fix_wanted(status[(int64_t)s * nprob + p], check_const))
+                    flagged[atomicAdd(&nflag, 1)] = s * nprob + p;
             }
         }
         __syncthreads();
@@ -1138,26 +1198,13 @@ __global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t s
         for (int f = 0; f < nf; ++f) {
             const int sp = flagged[f];
             const int s = sp / nprob, p = sp - s * nprob;
-            const uint32_t st = status[(int64_t)s * nprob + p];
-            if (check_const && (st & FM_ST_CONST_SUSPECT)) {
-                const_pair(s, p, sm.red, cols, stride, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
-                           prob_nz, status);
-                __syncthreads();
-            }
-            if (!(st & FM_ST_FITTED)) continue;
-            if (st & FM_ST_INF_IN_Y) {
-                infy_pair(s, p, sm.infy, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back,
-                          level, nprob, prob_level, prob_z, prob_nz, moments, mom_stride, pmax, rec);
-            } else if ((st & FM_ST_REFIT) && !(st & FM_ST_INF_IN_X) && prob_nz[p] <= NC) {
-                refit_pair<NC>(s, p, sm.refit, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale,
-                               add_back, level, nprob, prob_level, prob_z, prob_nz, pmax, rec, status);
-            } else {
-                continue;
-            }
-            __syncthreads();   // sm is reused by the next pair
+            fix_one<NC, VT>(s, p, status[(int64_t)s * nprob + p], sm, cols, stride, seg_off, nseg, lo, hi, shift,
+                            inv_scale, add_back, level, nprob, prob_level, prob_z, prob_nz, moments, mom_stride,
+                            pmax, rec, status, check_const);
         }
         __syncthreads();   // the list is rebuilt for the next range
     }
+    FM_PROBE_AT(solve, 5);
 }
 
 }  // namespace
@@ -1178,6 +1225,11 @@ extern "C" int fm_solve(const fm_solve_args* args, void* stream) {
     FM_REQUIRE(a.add_back == nullptr || (a.ab_ncols >= 1 && a.ab_ncols <= FM_MAX_COLS),
                "fm_solve: add_back needs ab_ncols in 1..%d", FM_MAX_COLS);
     FM_REQUIRE(a.zw == 32 || a.nprob <= S16_MAXP, "fm_solve: at most %d problems per group", S16_MAXP);
+    FM_REQUIRE(a.fix_cols == nullptr || (a.zw == 16 && a.fix_seg_off && a.moments && a.pmax + 1 <= 16 &&
+                                         (a.fix_lo == nullptr) == (a.fix_hi == nullptr) &&
+                                         (a.fix_inv_scale == nullptr || a.fix_shift != nullptr)),
+               "fm_solve: inline fix-ups need zw 16, fix_seg_off, moments, pmax <= 15, lo with hi, "
+               "shift with inv_scale");
     if (a.nseg == 0 || a.nprob == 0) return FM_OK;
     const size_t dyn = (size_t)a.npatterns * a.nlevels * (a.zw * (a.zw + 1) / 2) * sizeof(double);
     static bool attr_set = false;

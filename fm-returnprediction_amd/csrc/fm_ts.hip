@@ -21,6 +21,8 @@
 
 #include "fm_common.h"
 
+FM_PROBE_BUFFER(ts)
+
 namespace fm {
 namespace {
 
@@ -715,6 +717,7 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
         }
     }
     __syncthreads();
+    FM_PROBE_AT(ts, 2);
     // dropna in place, month order kept (each pass reads its span before any write lands)
     int n = 0;
     for (int i0 = 0; i0 < cnt; i0 += FT) {
@@ -735,6 +738,7 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
         n += tot;
         __syncthreads();
     }
+    FM_PROBE_AT(ts, 3);
     double sum = 0.0;
     for (int i = tid; i < n; i += FT) sum += xs[i];
     sum = block_sum<FNW>(sum, dred);
@@ -780,6 +784,7 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
         }
         acc += wgt * gk;
     }
+    FM_PROBE_AT(ts, 4);
     if (tid == 0) {
         const int64_t o = (int64_t)p * a.kmax + k;
         double se = NAN;
@@ -789,6 +794,138 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
         a.tstat[o] = mu / se;
         a.nobs[o] = n;
     }
+}
+
+// ts_summary_wg restated for ONE wave (the predictive summary of the last rolling workgroup,
+// one coefficient per wave): the block version's FT threads become this wave's lanes x FNW
+// virtual slots, each slot's partial sums taken and combined in the block version's order,
+// so the result bits are the same.
+__device__ void ts_summary_wave(const fm_ts_args& a, int p, int k, const int* ixs, int cnt, double* xs) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const double* rk = a.rec + (int64_t)p * a.r_prob + k;
+    for (int i0 = 0; i0 < cnt; i0 += 8 * WAVE) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int i = i0 + q * WAVE + lane;
+            v[q] = rk[(int64_t)ixs[i < cnt ? i : cnt - 1] * a.r_seg];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int i = i0 + q * WAVE + lane;
+            if (i < cnt) xs[i] = v[q];
+        }
+    }
+    wave_sync();
+    int n = 0;   // dropna in place, month order kept (a pass reads its span before writing)
+    for (int i0 = 0; i0 < cnt; i0 += WAVE) {
+        const int i = i0 + lane;
+        const double x = i < cnt ? xs[i] : NAN;
+        const bool v = !isnan(x);
+        const uint64_t bm = __ballot(v);
+        wave_sync();
+        if (v) xs[n + mask_rank(bm)] = x;
+        n += (int)__popcll(bm);
+        wave_sync();
+    }
+    double sq[FNW];
+#pragma unroll
+    for (int q = 0; q < FNW; ++q) {
+        sq[q] = 0.0;
+        for (int i = q * WAVE + lane; i < n; i += FT) sq[q] += xs[i];
+    }
+    double sum = wave_sum(sq[0]);
+#pragma unroll
+    for (int q = 1; q < FNW; ++q) sum += wave_sum(sq[q]);
+    const double mu = n > 0 ? sum / (double)n : NAN;
+    const int lags = a.nw_lags < MAXL ? a.nw_lags : MAXL;
+    double gl[MAXL + 1];
+#pragma unroll
+    for (int L = 0; L <= MAXL; ++L) gl[L] = 0.0;
+#pragma unroll
+    for (int q = 0; q < FNW; ++q) {
+        double g[MAXL + 1];
+#pragma unroll
+        for (int L = 0; L <= MAXL; ++L) g[L] = 0.0;
+        for (int i = q * WAVE + lane; i < n; i += FT) {
+            const double ui = xs[i] - mu;
+#pragma unroll
+            for (int L = 0; L <= MAXL; ++L)
+                if (L <= lags && i >= L) g[L] += ui * (xs[i - L] - mu);
+        }
+#pragma unroll
+        for (int L = 0; L <= MAXL; ++L) gl[L] += wave_sum(g[L]);   // t = 0 + d_0 + d_1 + ...
+    }
+    double acc = 0.0;
+    for (int L = 1; L <= a.nw_lags; ++L) {
+        const double wgt = 1.0 - ((double)L / (double)n);
+        if (wgt < 0.0) break;
+        double gk = 0.0;
+        if (L <= MAXL) {
+#pragma unroll
+            for (int q = 1; q <= MAXL; ++q)
+                if (q == L) gk = gl[q];
+        } else {
+            double t[FNW];
+#pragma unroll
+            for (int q = 0; q < FNW; ++q) {
+                t[q] = 0.0;
+                for (int i = L + q * WAVE + lane; i < n; i += FT) t[q] += (xs[i] - mu) * (xs[i - L] - mu);
+            }
+            gk = wave_sum(t[0]);
+#pragma unroll
+            for (int q = 1; q < FNW; ++q) gk += wave_sum(t[q]);
+        }
+        acc += wgt * gk;
+    }
+    if (lane == 0) {
+        const int64_t o = (int64_t)p * a.kmax + k;
+        double se = NAN;
+        if (n >= 2) se = sqrt((gl[0] + 2.0 * acc) / ((double)n * (double)n));
+        a.mean[o] = mu;
+        a.se[o] = se;
+        a.tstat[o] = mu / se;
+        a.nobs[o] = n;
+    }
+}
+
+// Last rolling workgroup of problem p (a.psum_ctr): the FM summary of p's predictive records,
+// as the separate fm_ts_fused launch on them would compute it; the counter is left at zero.
+__device__ void ts_pred_summary_last(const fm_ts_args& a, int p, int nchunk, int* ixs, double* lds_d,
+                                     int* wtot) {
+    __shared__ int last;
+    __syncthreads();   // every pred / pred_status write of this workgroup is issued
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t t = atomicAdd(&a.psum_ctr[p], 1u);
+        last = t == (uint32_t)nchunk - 1;
+        if (last) {
+            __hip_atomic_store(&a.psum_ctr[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence();
+        }
+    }
+    __syncthreads();
+    if (!last) return;   // block-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other workgroups' records
+    fm_ts_args b = a;
+    b.rec = a.pred;
+    b.r_seg = 4;
+    b.r_prob = (int64_t)a.nseg * 4;
+    b.status = a.pred_status;
+    b.s_seg = 1;
+    b.s_prob = a.nseg;
+    b.kmax = 3;
+    b.idx = a.psum_idx;
+    b.count = a.psum_count;
+    b.mean = a.psum_mean;
+    b.se = a.psum_se;
+    b.tstat = a.psum_tstat;
+    b.nobs = a.psum_nobs;
+    const int cnt = ts_compact_lds(b, p, ixs, wtot);
+    for (int i = threadIdx.x; i < cnt; i += FT) b.idx[(int64_t)p * b.nseg + i] = ixs[i];
+    if (threadIdx.x == 0) b.count[p] = cnt;
+    const int w = threadIdx.x / WAVE;
+    for (int k = w; k < b.kmax; k += FNW) ts_summary_wave(b, p, k, ixs, cnt, lds_d + (int64_t)w * a.nseg);
 }
 
 __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* ixs, int cnt,
@@ -840,6 +977,7 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
         }
     }
     __syncthreads();
+    FM_PROBE_AT(ts, 2);
     // per-column inclusive prefix sums of the finite values and their counts over the staged
     // rows (each output is then a difference of two prefixes: no serial window sums).  A
     // column's rows are split over 16 threads: local scans, then the 16 block totals.  The
@@ -870,17 +1008,17 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
         // exclusive prefix of the 16 part totals (lanes of one 16-lane row group)
         CSum bs = sm;
         int bc = cn;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const double yh = __shfl_up(bs.s, o, 16);
-            const double yl = __shfl_up(bs.c, o, 16);
-            const int yc = __shfl_up(bc, o, 16);
+        static_for<0, 4>([&](auto oc) {
+            constexpr int o = 1 << decltype(oc)::value;
+            const double yh = row_shr<o>(bs.s);
+            const double yl = row_shr<o>(bs.c);
+            const int yc = row_shr<o>(bc);
             if (part >= o) {
                 bs.add(yh);
                 bs.c += yl;
                 bc += yc;
             }
-        }
+        });
         bs.add(-sm.s);
         bs.c -= sm.c;
         bc -= cn;
@@ -894,6 +1032,7 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
             }
     }
     __syncthreads();
+    FM_PROBE_AT(ts, 3);
     for (int e = tid; e < nq * PM; e += FT) {
         const int q = e / PM, k = e - q * PM, i = q0 + q;
         const int jlo = i - a.window;                 // prefix just before the window
@@ -912,6 +1051,7 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
     }
     if (!predictive) return;
     __syncthreads();
+    FM_PROBE_AT(ts, 4);
     // predictive slopes: a 16-lane group per row, lane b owns column b of each S row
     const int K = a.prob_k[p], K1 = K + 1;
     const int g = tid >> 4, b = tid & 15;
@@ -938,6 +1078,7 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
             syq[it] = S[K * K1 + K];
         }
     }
+    FM_PROBE_AT(ts, 5);
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {     // uniform trip count (shuffles)
         const int i = r0 + g + it * (FT / 16);
@@ -987,11 +1128,8 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
                 }
             }
         }
-#pragma unroll
-        for (int m = 8; m >= 1; m >>= 1) {
-            tb += __shfl_xor(tb, m, 16);
-            ty += __shfl_xor(ty, m, 16);
-        }
+        tb = row16_sum(tb);
+        ty = row16_sum(ty);
         if (row && b == 0) {
             double* o = a.pred + ((int64_t)p * T + i) * 4;
             uint32_t st = 0;
@@ -1022,13 +1160,21 @@ __global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {
     const int p = blockIdx.y, bx = blockIdx.x;
     int* ixs = reinterpret_cast<int*>(lds);
     double* lds_d = lds + ts_ix_bytes(a.nseg) / 8;
+    FM_PROBE_AT(ts, 0);
     const int cnt = ts_compact_lds(a, p, ixs, wtot);
+    FM_PROBE_AT(ts, 1);
     if (bx == 0) {
         for (int i = threadIdx.x; i < cnt; i += FT) a.idx[(int64_t)p * a.nseg + i] = ixs[i];
         if (threadIdx.x == 0) a.count[p] = cnt;
     }
-    if (bx < a.kmax) ts_summary_wg(a, p, bx, ixs, cnt, lds_d, wtot, dred);
-    else ts_rolling_wg(a, p, bx - a.kmax, ixs, cnt, lds_d);
+    if (bx < a.kmax) {
+        ts_summary_wg(a, p, bx, ixs, cnt, lds_d, wtot, dred);
+    } else {
+        ts_rolling_wg(a, p, bx - a.kmax, ixs, cnt, lds_d);
+        FM_PROBE_AT(ts, 6);
+        if (a.psum_mean != nullptr) ts_pred_summary_last(a, p, (int)gridDim.x - a.kmax, ixs, lds_d, wtot);
+    }
+    FM_PROBE_AT(ts, 7);
 }
 
 }  // namespace
@@ -1060,8 +1206,14 @@ extern "C" int fm_ts_fused(const fm_ts_args* args, void* stream) {
     FM_REQUIRE(a.pred == nullptr || (a.roll && a.moments && a.prob_k && a.pred_status && a.lag >= 1),
                "fm_ts_fused: the predictive stage needs roll, moments, prob_k, pst and lag >= 1");
     if (a.nprob == 0 || a.nseg == 0) return FM_OK;
-    const size_t lds = fm_ts_fused_lds_bytes(a.nseg, a.pmax, a.window, a.lag, a.roll != nullptr,
-                                             a.pred != nullptr);
+    FM_REQUIRE(a.psum_mean == nullptr || (a.pred && a.psum_idx && a.psum_count && a.psum_se && a.psum_tstat &&
+                                           a.psum_nobs && a.psum_ctr),
+               "fm_ts_fused: the predictive summary needs pred and every psum_* buffer");
+    size_t lds = fm_ts_fused_lds_bytes(a.nseg, a.pmax, a.window, a.lag, a.roll != nullptr, a.pred != nullptr);
+    if (a.psum_mean != nullptr) {   // the last rolling workgroup stages one series per wave
+        const size_t ps = ts_ix_bytes(a.nseg) + (size_t)FNW * a.nseg * 8;
+        lds = lds > ps ? lds : ps;
+    }
     FM_REQUIRE(lds <= FM_TS_FUSED_MAX_LDS,
                "fm_ts_fused: series too long for LDS staging (use the per-stage entry points)");
     if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit: opt in (once)

@@ -72,6 +72,9 @@ class TsArgs(C.Structure):
         ("work", _p), ("window", _i32), ("min_periods", _i32), ("pmax", _i32), ("roll", _p),
         ("moments", _p), ("mom_stride", _i32), ("prob_k", _p), ("lag", _i32), ("seg_lo", _i32),
         ("seg_hi", _i32), ("pred", _p), ("pred_status", _p),
+        # the predictive records' summary in the same launch (psum_mean None: not here)
+        ("psum_idx", _p), ("psum_count", _p), ("psum_mean", _p), ("psum_se", _p), ("psum_tstat", _p),
+        ("psum_nobs", _p), ("psum_ctr", _p),
     ]
 
 
@@ -83,6 +86,10 @@ class SolveArgs(C.Structure):
         ("prob_nz", _p), ("prob_flags", _p), ("add_back", _p), ("gram_flags", _p),
         ("nmodels", _i32), ("pmax", _i32), ("rec", _p), ("status", _p),
         ("moments", _p), ("mom_stride", _i32), ("ab_ncols", _i32),
+        # inline statsmodels fix-ups (fix_cols None: a separate fm_solve_fixup call)
+        ("fix_cols", _p), ("fix_stride", _i64), ("fix_seg_off", _p), ("fix_lo", _p), ("fix_hi", _p),
+        ("fix_shift", _p), ("fix_inv_scale", _p), ("fix_level", _p), ("fix_check_const", _i32),
+        ("fix_pad", _i32),
     ]
 
 

@@ -695,12 +695,22 @@ def _solve_group(panel, src, gpl, partial, seg_chunk_off, zw, nlevels, T, pmax, 
         prob_nz=gpl.pnz.data_ptr(), prob_flags=gpl.pf.data_ptr(), add_back=_ptr(add_back),
         gram_flags=None, nmodels=gpl.nmodels, pmax=pmax, rec=grec.data_ptr(),
         status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride, ab_ncols=src.shape[0])
+    # statsmodels fix-ups: the exact nonzero-constant test where the solve saw a near-zero
+    # variance (CONST_SUSPECT), inf in y (pinv(X) @ y gives +-inf / NaN coefficients) and the
+    # QR + SVD refit of ill-conditioned / rank-deficient problems (FM_ST_REFIT).  The 16-wide
+    # solve does them inside its own launch (each month's workgroup, right after its solve);
+    # the 32-wide one is followed by fm_solve_fixup, which scans the status on the device
+    # (npairs = -1): no host round trip either way.
+    inline_fix = zw == 16 and pmax + 1 <= 16
+    if inline_fix:
+        sa.fix_cols, sa.fix_stride, sa.fix_seg_off = src.data_ptr(), src.stride(0), panel.seg_off.data_ptr()
+        sa.fix_lo, sa.fix_hi, sa.fix_shift, sa.fix_inv_scale = _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale)
+        sa.fix_level, sa.fix_check_const = _ptr(level), int(bool(const_check))
     _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
-    _remember("fm_solve", "fm_solve", sa, partial, seg_chunk_off, gpl, add_back, grec, gst, gmom, *keep)
-    # statsmodels fix-ups in one launch: the exact nonzero-constant test where the solve saw a
-    # near-zero variance (CONST_SUSPECT), inf in y (pinv(X) @ y gives +-inf / NaN
-    # coefficients) and the QR + SVD refit of ill-conditioned / rank-deficient problems
-    # (FM_ST_REFIT).  It scans the status on the device (npairs = -1): no host round trip.
+    _remember("fm_solve", "fm_solve", sa, partial, seg_chunk_off, gpl, add_back, grec, gst, gmom, src, lo, hi,
+              shift, inv_scale, level, *keep)
+    if inline_fix:
+        return grec, gst, gmom
     _kcall("fm_solve_fixup", "fm_solve_fixup", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
            _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), ng,
            gpl.pl.data_ptr(), gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1,
@@ -896,12 +906,33 @@ def ts_fused_fits(nseg, pmax=0, window=None, lag=1, predictive=False):
     return need <= L.FM_TS_FUSED_MAX_LDS
 
 
+_PSUM_CTR = {}
+
+
+def _psum_ctr(dev, nprob):
+    """Arrival counters of fm_ts_fused's in-launch predictive summary: zeroed once, every
+    launch leaves them zero (one buffer per device and problem count, reused by the graphs)."""
+    key = (str(dev), nprob)
+    if key not in _PSUM_CTR:
+        _PSUM_CTR[key] = torch.zeros(max(nprob, 1), dtype=torch.int32, device=dev)
+    return _PSUM_CTR[key]
+
+
+def ts_pred_summary_fits(nseg):
+    """Whether fm_ts_fused's last rolling workgroup can stage the predictive summary (one
+    series per wave in LDS)."""
+    return ((nseg * 4 + 15) & ~15) + 4 * nseg * 8 <= L.FM_TS_FUSED_MAX_LDS
+
+
 def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_lags=4,
              window=None, min_periods=None, pmax=None, moments=None, mom_stride=0, prob_k=None,
-             lag=1, seg_lo=0, seg_hi=None, predictive=False, tag="fm_ts_fused"):
+             lag=1, seg_lo=0, seg_hi=None, predictive=False, pred_summary=False, tag="fm_ts_fused"):
     """The whole time-series stage in one launch (fm_ts_fused): TSIndex, Summary and, when
     ``window`` is given, the rolling means [P, T, pmax]; with ``predictive`` also the
-    predictive records [P, T, 4] and status [P, T].  Returns (ix, summ, roll, pred, pst)."""
+    predictive records [P, T, 4] and status [P, T].  Returns (ix, summ, roll, pred, pst);
+    with ``pred_summary`` (predictive, no exchange before the summary) a sixth element, the
+    predictive records' (Summary, TSIndex) -- summarize_predictive's result, bit for bit --
+    from the same launch (each problem's last rolling workgroup)."""
     dev = rec.device
     idx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
     cnt = torch.empty(nprob, dtype=torch.int32, device=dev)
@@ -921,19 +952,38 @@ def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_la
                   min_periods=min_periods or 0, pmax=pmax or 0, roll=_ptr(roll), moments=_ptr(moments),
                   mom_stride=mom_stride, prob_k=_ptr(prob_k), lag=lag, seg_lo=seg_lo,
                   seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst))
+    psum, pbufs = None, ()
+    if pred_summary:
+        if not predictive:
+            raise ValueError("pred_summary needs predictive")
+        pidx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
+        pcnt = torch.empty(nprob, dtype=torch.int32, device=dev)
+        pmean = torch.empty((nprob, 3), dtype=torch.float64, device=dev)
+        pse, pts = torch.empty_like(pmean), torch.empty_like(pmean)
+        pnobs = torch.empty((nprob, 3), dtype=torch.int32, device=dev)
+        ctr = _psum_ctr(dev, nprob)
+        ta.psum_idx, ta.psum_count, ta.psum_mean = pidx.data_ptr(), pcnt.data_ptr(), pmean.data_ptr()
+        ta.psum_se, ta.psum_tstat, ta.psum_nobs, ta.psum_ctr = (pse.data_ptr(), pts.data_ptr(), pnobs.data_ptr(),
+                                                                 ctr.data_ptr())
+        psum = (Summary(pmean, pse, pts, pnobs), TSIndex(pidx, pcnt))
+        pbufs = (pidx, pcnt, pmean, pse, pts, pnobs, ctr)
     _kcall(tag, "fm_ts_fused", L.C.byref(ta), _stream())
     _remember(tag, "fm_ts_fused", ta, rec, status, idx, cnt, mean, se, ts, nobs, roll,
-              moments, prob_k, pred, pst)
-    return TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst
+              moments, prob_k, pred, pst, *pbufs)
+    out = (TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst)
+    return out + (psum,) if pred_summary else out
 
 
 def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag=1, seg_lo=0,
-                       seg_hi=None, moments=None, rolling=True, predictive=True):
+                       seg_hi=None, moments=None, rolling=True, predictive=True, pred_summary=False):
     """compact_result + summarize_result + rolling_result + predictive_result in one launch.
-    Returns (ix, summ, roll, pred, pst)."""
+    Returns (ix, summ, roll, pred, pst); with ``pred_summary`` (predictive runs without an
+    exchange of the predictive records) also the predictive (Summary, TSIndex) as a sixth
+    element, from the same launch where it fits."""
     T, P, rs = res.rec.shape
     mom = res.moments if moments is None else moments
     window = window if (rolling or predictive) else None
+    pred_summary = bool(pred_summary and predictive)
     if not ts_fused_fits(T, res.pmax, window, lag, predictive):
         ix = compact_result(res)
         summ, _ = summarize_result(res, ix, nw_lags)
@@ -942,12 +992,17 @@ def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag
             roll = rolling_result(res, ix, window, min_periods)
         if predictive:
             pred, pst = predictive_result(res, ix, roll, lag, seg_lo, seg_hi, moments)
-        return ix, summ, roll, pred, pst
+        out = (ix, summ, roll, pred, pst)
+        return out + (summarize_predictive(pred, pst, nw_lags),) if pred_summary else out
     pk = _small_tensor(tuple(p.K for p in res.problems), torch.int32, res.rec.device) if predictive else None
-    return ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
-                    window=window, min_periods=min_periods,
-                    pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
-                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive)
+    fold = pred_summary and ts_pred_summary_fits(T)
+    out = ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
+                   window=window, min_periods=min_periods,
+                   pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
+                   prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive, pred_summary=fold)
+    if pred_summary and not fold:
+        out = out + (summarize_predictive(out[3], out[4], nw_lags),)
+    return out
 
 
 def forecast(panel: DevicePanel, coef, cols=None):

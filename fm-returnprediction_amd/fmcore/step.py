@@ -65,8 +65,11 @@ class ShardedStep:
         if self.exchange:
             gres = E.FMResult(problems=res.problems, rec=self.rec_g, status=self.st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
-        ix, summ, roll, pred, pst = LW.time_series_stage(gres, self.cfg, moments=res.moments,
-                                                         seg_lo=self.seg_lo, seg_hi=self.seg_hi)
+        # without an exchange of the predictive records the launch also gives their summary
+        ix, summ, roll, pred, pst, ps = LW.time_series_stage(gres, self.cfg, moments=res.moments,
+                                                             seg_lo=self.seg_lo, seg_hi=self.seg_hi,
+                                                             pred_summary=not self.exchange)
+        self._psum = ps
         return gres, summ, pred, pst
 
     def exchange_pred(self, pred, pst):
@@ -76,6 +79,8 @@ class ShardedStep:
     def phase_pred(self, pred, pst):
         if pred is None:
             return None
+        if not self.exchange and getattr(self, "_psum", None) is not None:
+            return self._psum[0]   # came with phase_ts's launch
         psumm, _ = E.summarize_predictive(pred, pst, self.cfg.nw_lags)
         return psumm
 

@@ -162,6 +162,21 @@ typedef struct fm_solve_args {
     double* moments;              /* [nseg][nprob][mom_stride] or NULL: n, means(K+1), centered (K+1)^2 */
     int32_t mom_stride;
     int32_t ab_ncols;             /* rows of add_back ([ab_ncols][nseg]; the panel's ncols) */
+    /* The statsmodels fix-ups of fm_solve_fixup (npairs = -1) inside this launch, by each
+     * month's own workgroup right after its solve (zw 16 only; fix_cols NULL -- the
+     * zero-initialised default -- leaves them to a separate fm_solve_fixup call).  The
+     * arguments are fm_solve_fixup's: the panel columns the Gram read, its cuts, standardizing
+     * shift / scale, universe levels; moments must be set. */
+    const double* fix_cols;
+    int64_t fix_stride;
+    const int64_t* fix_seg_off;
+    const double* fix_lo;
+    const double* fix_hi;
+    const double* fix_shift;
+    const double* fix_inv_scale;
+    const uint8_t* fix_level;
+    int32_t fix_check_const;
+    int32_t fix_pad;
 } fm_solve_args;
 
 const char* fm_version(void);
@@ -344,6 +359,18 @@ typedef struct fm_ts_args {
     int32_t lag, seg_lo, seg_hi;
     double* pred;                 /* [nprob][nseg][4] or NULL */
     uint32_t* pred_status;        /* [nprob][nseg] */
+    /* The predictive records' FM summary inside this launch (runs with no exchange between
+     * the two stages): with psum_mean set (pred set too), the last rolling workgroup of each
+     * problem compacts its pred_status and summarizes the first 3 fields of its pred records
+     * -- what fm_ts_fused on (pred, 4, nseg*4, pred_status, 1, nseg, nseg, nprob, kmax 3)
+     * returns, bit for bit.  All NULL (zero-initialised): no predictive summary here. */
+    int32_t* psum_idx;            /* [nprob][nseg] */
+    int32_t* psum_count;          /* [nprob] */
+    double* psum_mean;            /* [nprob][3] */
+    double* psum_se;
+    double* psum_tstat;
+    int32_t* psum_nobs;
+    uint32_t* psum_ctr;           /* [nprob] arrival counters: zero before the first launch, left zero */
 } fm_ts_args;
 
 /* LDS bytes the fused launch stages per workgroup; it must not exceed FM_TS_FUSED_MAX_LDS

@@ -21,6 +21,7 @@ for s in "$@"; do
     split)   specs+=("split:::300:::python tools/split_scan.py");;
     rehearse) specs+=("rehearse:::400:::python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --one-device --c5-months 400 --months 300");;
     spawn)   specs+=("spawn:::400:::python bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --one-device --c5-months 400 --months 300 --no-headline");;
+    tprobe)  specs+=("tprobe:::200:::FM_HIP_LIB=$R/build_variants/probe/libfm_hip.so python tools/tail_probe.py");;
     wgtime)  specs+=("wgtime:::200:::FM_HIP_LIB=$R/build_variants/wgtime/libfm_hip.so python tools/gram_wgtime.py");;
     kbench)  specs+=("kbench:::300:::python tools/kbench.py $KB_LIBS");;
     slab)    specs+=("slab:::300:::python tools/slab_probe.py");;
