@@ -19,9 +19,9 @@
 
 #include "fm_common.h"
 
-#include "fm_select_dev.h"
-
 FM_PROBE_BUFFER(sel)
+#define FM_HS_PROBE_ON 1
+#include "fm_select_dev.h"
 #include "fm_npsel_dev.h"
 
 #ifndef FM_SELECT_STREAM_VPT
@@ -1850,9 +1850,27 @@ __global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const d
             kmx = k > kmx ? k : kmx;
         }
     });
-    const int n = block_sum<SNW>(cnt, sm.ints);
-    kmn = block_min_u64<SNW>(kmn, sm.u64s);
-    kmx = block_max_u64<SNW>(kmx, sm.u64s + SNW);
+    // count, min and max in one exchange (one barrier; nothing of sm is in use yet)
+    {
+        const int c = wave_sum(cnt);
+        const uint64_t mn = wave_min_u64(kmn), mx = wave_max_u64(kmx);
+        const int w = tid / WAVE;
+        if ((tid & (WAVE - 1)) == 0) {
+            sm.ints[w] = c;
+            sm.u64s[w] = mn;
+            sm.u64s[SNW + w] = mx;
+        }
+    }
+    __syncthreads();
+    int n = sm.ints[0];
+    kmn = sm.u64s[0];
+    kmx = sm.u64s[SNW];
+#pragma unroll
+    for (int q = 1; q < SNW; ++q) {
+        n += sm.ints[q];
+        kmn = sm.u64s[q] < kmn ? sm.u64s[q] : kmn;
+        kmx = sm.u64s[SNW + q] > kmx ? sm.u64s[SNW + q] : kmx;
+    }
     double a = NAN, b = NAN;
     FM_PROBE_AT(sel, 1);
     if (n > 0) {   // block-uniform

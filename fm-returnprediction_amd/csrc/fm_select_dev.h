@@ -375,6 +375,14 @@ __device__ __forceinline__ void wave_sort_lds(uint64_t* buf, int c) {
 // `for_each(f)` calls f(x) for each of this thread's values (NaN = absent): register-resident
 // values or a grid-stride stream over HBM (long segments), the same code either way.  n,
 // kmin, kmax describe the non-NaN values; block-uniform control flow; barriers inside.
+// probe builds of fm_select.hip only (tools/tail_probe.py): phase marks of hist_select
+#if FM_PROBE && defined(FM_HS_PROBE_ON)
+#define FM_HS_PROBE(slot) FM_PROBE_AT(sel, slot)
+#else
+#define FM_HS_PROBE(slot) \
+    do {                  \
+    } while (0)
+#endif
 template <int NW, int HBN, int CAP, typename Sm, typename ForEach>
 __device__ __forceinline__ void hist_select_t(ForEach&& for_each, int nr, const int* rk, uint64_t kmin,
                                               uint64_t kmax, uint64_t* out, Sm& sm) {
@@ -450,6 +458,7 @@ __device__ __forceinline__ void hist_select_t(ForEach&& for_each, int nr, const 
             }
         });
         __syncthreads();
+        FM_HS_PROBE(4);
         // block scan: thread tid owns bins [8 tid, 8 tid + 8)
         constexpr int BPT = HBN / NT;
         uint32_t h[BPT];
@@ -473,6 +482,7 @@ __device__ __forceinline__ void hist_select_t(ForEach&& for_each, int nr, const 
             run += (int)h[j];
         }
         __syncthreads();
+        FM_HS_PROBE(5);
         uint64_t blo[4], bhi[4];
         int lst[4], lrank[4], lcnt[4];
         bool any_list = false;
@@ -538,6 +548,7 @@ __device__ __forceinline__ void hist_select_t(ForEach&& for_each, int nr, const 
             }
         });
         __syncthreads();
+        FM_HS_PROBE(6);
         for (int w = tid / WAVE; w < nl; w += NW) {   // one wave per list
             const int c = (int)sm.hcnt[w];
             uint64_t* L = sm.buf + w * CAP;
@@ -546,6 +557,7 @@ __device__ __forceinline__ void hist_select_t(ForEach&& for_each, int nr, const 
             else wave_sort_lds<(CAP > 2 * WAVE ? 4 : 2)>(L, c);
         }
         __syncthreads();
+        FM_HS_PROBE(7);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             if (lst[t] >= 0) {

@@ -532,6 +532,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
                 row[j] = 0.0;
             }
         });
+        FM_PROBE_AT(solve, 4);
         const double mu = G[0] * ninv;   // lane i: mean of its variable
         const uint64_t gm = 0xFFFFull << (16 * g);
         uint32_t st = 0;
@@ -568,6 +569,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
             if (live && i == 0) a.rec[ro] = row[0] + row[1] + mu;
             continue;
         }
+        FM_PROBE_AT(solve, 5);
         // ---- augmented Cholesky of S (pivot r = k sits in lane k + 1)
         bool ok = act0, illc = false;
         double dinv = 0.0;   // lane k + 1: 1 / L[k][k] (the back substitution multiplies by it)
@@ -593,6 +595,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
             row[k] = go ? (i == k + 1 ? lkk : lik) : row[k];
             dinv = i == k + 1 ? rinv : dinv;
         });
+        FM_PROBE_AT(solve, 6);
         // lanes of a live, unskipped problem with a collapsed pivot: rank deficient
         const bool rank_def = act0 && !ok;
         // ---- back substitution L' b = l on the transposed factor: lane i then holds
@@ -622,6 +625,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        FM_PROBE_AT(solve, 7);
         double bi = (ok && i >= 1 && i <= K) ? t : 0.0;   // slope of x_{i-1}
         // ---- rank-deficient problems of this wave: Jacobi pseudo-inverse, one at a time
         const uint64_t rd = __ballot(rank_def && i == 0);
@@ -784,7 +788,7 @@ struct InfySmem {
     int okf;
 };
 
-template <int NT = VT>
+template <int NT = VT, int NC = 32>
 __device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, const double* cols, int64_t stride,
                                           const int64_t* seg_off, int nseg, const double* lo,
                                           const double* hi, const double* shift,
@@ -829,6 +833,71 @@ __device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, const doub
     __syncthreads();
     if (!okf) return;   // rank-deficient with an inf y: left as computed (NaN)
     const int64_t r0 = seg_off[s], r1 = seg_off[s + 1];
+    if constexpr (NC <= 16) {
+        // register arrays (fully unrolled, statically indexed: no scratch, which would throttle
+        // the waves of the solve kernel these fix-ups ride); the opaque zero keeps the factor's
+        // LDS reads inside the row loop instead of hoisted into ~120 live registers
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += NT) {
+            if (level && (int)level[r] < u) continue;
+            int zo = 0;
+            asm volatile("" : "+v"(zo));
+            double d[NC];
+            double y = 0.0;
+            bool valid = true;
+#pragma unroll
+            for (int q = 1; q <= NC; ++q) {
+                if (q < nz) {
+                    const int c = zi[q] - 1;
+                    double x = cols[(int64_t)c * stride + r];
+                    if (lo) {
+                        const double l = lo[(int64_t)c * nseg + s], h = hi[(int64_t)c * nseg + s];
+                        if (x < l) x = l;
+                        if (x > h) x = h;
+                    }
+                    if (isnan(x)) valid = false;
+                    if (q == nz - 1) {
+                        y = x;
+                    } else {
+                        if (shift) x -= shift[(int64_t)c * nseg + s];
+                        if (inv_scale) x *= inv_scale[(int64_t)c * nseg + s];
+                        d[q - 1] = x - mu[q - 1 + zo];
+                    }
+                }
+            }
+            if (!valid || !isinf(y)) continue;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {          // L w = d
+                if (i < K) {
+                    double t = d[i];
+#pragma unroll
+                    for (int j = 0; j < i; ++j) t -= Lm[i * 32 + j + zo] * d[j];
+                    d[i] = t / Lm[i * 32 + i + zo];
+                }
+            }
+#pragma unroll
+            for (int i = NC - 1; i >= 0; --i) {     // L' c = w
+                if (i < K) {
+                    double t = d[i];
+#pragma unroll
+                    for (int j = i + 1; j < NC; ++j)
+                        if (j < K) t -= Lm[j * 32 + i + zo] * d[j];
+                    d[i] = t / Lm[i * 32 + i + zo];
+                }
+            }
+            double c0 = 1.0 / n;
+#pragma unroll
+            for (int j = 0; j < NC; ++j)
+                if (j < K) c0 -= xb[j + zo] * d[j];
+#pragma unroll
+            for (int j = 0; j <= NC; ++j) {
+                if (j <= K) {
+                    const double term = (j == 0 ? c0 : d[j == 0 ? 0 : j - 1]) * y;
+                    const unsigned b = isnan(term) ? 4u : (term > 0.0 ? 1u : 2u);
+                    atomicOr(&bits[j], b);
+                }
+            }
+        }
+    } else
     for (int64_t r = r0 + threadIdx.x; r < r1; r += NT) {
         if (level && (int)level[r] < u) continue;
         double v[32];
@@ -1144,7 +1213,7 @@ __device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, N
     }
     if (!(st & FM_ST_FITTED)) return;
     if (st & FM_ST_INF_IN_Y) {
-        infy_pair<NT>(s, p, sm.infy, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level,
+        infy_pair<NT, NC>(s, p, sm.infy, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level,
                       nprob, prob_level, prob_z, prob_nz, moments, mom_stride, pmax, rec);
     } else if ((st & FM_ST_REFIT) && !(st & FM_ST_INF_IN_X) && prob_nz[p] <= NC) {
         refit_pair<NC, NT>(s, p, sm.refit, cols, stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back,

@@ -796,117 +796,25 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
     }
 }
 
-// ts_summary_wg restated for ONE wave (the predictive summary of the last rolling workgroup,
-// one coefficient per wave): the block version's FT threads become this wave's lanes x FNW
-// virtual slots, each slot's partial sums taken and combined in the block version's order,
-// so the result bits are the same.
-__device__ void ts_summary_wave(const fm_ts_args& a, int p, int k, const int* ixs, int cnt, double* xs) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const double* rk = a.rec + (int64_t)p * a.r_prob + k;
-    for (int i0 = 0; i0 < cnt; i0 += 8 * WAVE) {
-        double v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int i = i0 + q * WAVE + lane;
-            v[q] = rk[(int64_t)ixs[i < cnt ? i : cnt - 1] * a.r_seg];
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int i = i0 + q * WAVE + lane;
-            if (i < cnt) xs[i] = v[q];
-        }
-    }
-    wave_sync();
-    int n = 0;   // dropna in place, month order kept (a pass reads its span before writing)
-    for (int i0 = 0; i0 < cnt; i0 += WAVE) {
-        const int i = i0 + lane;
-        const double x = i < cnt ? xs[i] : NAN;
-        const bool v = !isnan(x);
-        const uint64_t bm = __ballot(v);
-        wave_sync();
-        if (v) xs[n + mask_rank(bm)] = x;
-        n += (int)__popcll(bm);
-        wave_sync();
-    }
-    double sq[FNW];
-#pragma unroll
-    for (int q = 0; q < FNW; ++q) {
-        sq[q] = 0.0;
-        for (int i = q * WAVE + lane; i < n; i += FT) sq[q] += xs[i];
-    }
-    double sum = wave_sum(sq[0]);
-#pragma unroll
-    for (int q = 1; q < FNW; ++q) sum += wave_sum(sq[q]);
-    const double mu = n > 0 ? sum / (double)n : NAN;
-    const int lags = a.nw_lags < MAXL ? a.nw_lags : MAXL;
-    double gl[MAXL + 1];
-#pragma unroll
-    for (int L = 0; L <= MAXL; ++L) gl[L] = 0.0;
-#pragma unroll
-    for (int q = 0; q < FNW; ++q) {
-        double g[MAXL + 1];
-#pragma unroll
-        for (int L = 0; L <= MAXL; ++L) g[L] = 0.0;
-        for (int i = q * WAVE + lane; i < n; i += FT) {
-            const double ui = xs[i] - mu;
-#pragma unroll
-            for (int L = 0; L <= MAXL; ++L)
-                if (L <= lags && i >= L) g[L] += ui * (xs[i - L] - mu);
-        }
-#pragma unroll
-        for (int L = 0; L <= MAXL; ++L) gl[L] += wave_sum(g[L]);   // t = 0 + d_0 + d_1 + ...
-    }
-    double acc = 0.0;
-    for (int L = 1; L <= a.nw_lags; ++L) {
-        const double wgt = 1.0 - ((double)L / (double)n);
-        if (wgt < 0.0) break;
-        double gk = 0.0;
-        if (L <= MAXL) {
-#pragma unroll
-            for (int q = 1; q <= MAXL; ++q)
-                if (q == L) gk = gl[q];
-        } else {
-            double t[FNW];
-#pragma unroll
-            for (int q = 0; q < FNW; ++q) {
-                t[q] = 0.0;
-                for (int i = L + q * WAVE + lane; i < n; i += FT) t[q] += (xs[i] - mu) * (xs[i - L] - mu);
-            }
-            gk = wave_sum(t[0]);
-#pragma unroll
-            for (int q = 1; q < FNW; ++q) gk += wave_sum(t[q]);
-        }
-        acc += wgt * gk;
-    }
-    if (lane == 0) {
-        const int64_t o = (int64_t)p * a.kmax + k;
-        double se = NAN;
-        if (n >= 2) se = sqrt((gl[0] + 2.0 * acc) / ((double)n * (double)n));
-        a.mean[o] = mu;
-        a.se[o] = se;
-        a.tstat[o] = mu / se;
-        a.nobs[o] = n;
-    }
-}
+// The predictive records' FM summary inside the launch (a.psum_*): workgroup k of the PSK
+// extra workgroups of problem p summarizes field k of p's predictive records with the same
+// code as the separate launch on them (ts_compact_lds + ts_summary_wg: the same bits), once
+// every rolling workgroup of p has counted itself done in a.psum_ctr[p].  It waits only on
+// workgroups of lower linear id (dispatched before it), and fm_ts_fused folds the summary in
+// only when the whole grid is co-resident, so the wait always ends; the counter is reset by
+// the last of the PSK summary workgroups for the next launch.
+constexpr int PSK = 3;   // summarized fields of a predictive record (slope, R^2, n)
 
-// Last rolling workgroup of problem p (a.psum_ctr): the FM summary of p's predictive records,
-// as the separate fm_ts_fused launch on them would compute it; the counter is left at zero.
-__device__ void ts_pred_summary_last(const fm_ts_args& a, int p, int nchunk, int* ixs, double* lds_d,
-                                     int* wtot) {
-    __shared__ int last;
-    __syncthreads();   // every pred / pred_status write of this workgroup is issued
+__device__ void ts_pred_summary_wg(const fm_ts_args& a, int p, int k, int nroll, int* ixs, double* lds_d,
+                                   int* wtot, double* dred) {
     if (threadIdx.x == 0) {
-        __threadfence();
-        const uint32_t t = atomicAdd(&a.psum_ctr[p], 1u);
-        last = t == (uint32_t)nchunk - 1;
-        if (last) {
-            __hip_atomic_store(&a.psum_ctr[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __threadfence();
-        }
+        uint32_t spins = 0;   // bounded: a grid that drains is worth more than a hung one
+        while (__hip_atomic_load(&a.psum_ctr[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)nroll &&
+               ++spins < (1u << 24))
+            __builtin_amdgcn_s_sleep(2);
     }
     __syncthreads();
-    if (!last) return;   // block-uniform
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other workgroups' records
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the rolling workgroups' records
     fm_ts_args b = a;
     b.rec = a.pred;
     b.r_seg = 4;
@@ -914,7 +822,7 @@ __device__ void ts_pred_summary_last(const fm_ts_args& a, int p, int nchunk, int
     b.status = a.pred_status;
     b.s_seg = 1;
     b.s_prob = a.nseg;
-    b.kmax = 3;
+    b.kmax = PSK;
     b.idx = a.psum_idx;
     b.count = a.psum_count;
     b.mean = a.psum_mean;
@@ -922,10 +830,16 @@ __device__ void ts_pred_summary_last(const fm_ts_args& a, int p, int nchunk, int
     b.tstat = a.psum_tstat;
     b.nobs = a.psum_nobs;
     const int cnt = ts_compact_lds(b, p, ixs, wtot);
-    for (int i = threadIdx.x; i < cnt; i += FT) b.idx[(int64_t)p * b.nseg + i] = ixs[i];
-    if (threadIdx.x == 0) b.count[p] = cnt;
-    const int w = threadIdx.x / WAVE;
-    for (int k = w; k < b.kmax; k += FNW) ts_summary_wave(b, p, k, ixs, cnt, lds_d + (int64_t)w * a.nseg);
+    if (k == 0) {
+        for (int i = threadIdx.x; i < cnt; i += FT) b.idx[(int64_t)p * b.nseg + i] = ixs[i];
+        if (threadIdx.x == 0) b.count[p] = cnt;
+    }
+    ts_summary_wg(b, p, k, ixs, cnt, lds_d, wtot, dred);
+    if (threadIdx.x == 0) {   // every thread of this workgroup is past its read of the counter
+        const uint32_t t = atomicAdd(&a.psum_ctr[p], 1u);
+        if (t == (uint32_t)(nroll + PSK - 1))
+            __hip_atomic_store(&a.psum_ctr[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* ixs, int cnt,
@@ -1161,6 +1075,12 @@ __global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {
     int* ixs = reinterpret_cast<int*>(lds);
     double* lds_d = lds + ts_ix_bytes(a.nseg) / 8;
     FM_PROBE_AT(ts, 0);
+    const int nroll = a.roll ? (a.nseg + RROWS - 1) / RROWS : 0;
+    if (a.psum_mean != nullptr && bx >= a.kmax + nroll) {   // block-uniform
+        ts_pred_summary_wg(a, p, bx - a.kmax - nroll, nroll, ixs, lds_d, wtot, dred);
+        FM_PROBE_AT(ts, 7);
+        return;
+    }
     const int cnt = ts_compact_lds(a, p, ixs, wtot);
     FM_PROBE_AT(ts, 1);
     if (bx == 0) {
@@ -1172,7 +1092,13 @@ __global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {
     } else {
         ts_rolling_wg(a, p, bx - a.kmax, ixs, cnt, lds_d);
         FM_PROBE_AT(ts, 6);
-        if (a.psum_mean != nullptr) ts_pred_summary_last(a, p, (int)gridDim.x - a.kmax, ixs, lds_d, wtot);
+        if (a.psum_mean != nullptr) {   // this problem's predictive summary waits for the count
+            __syncthreads();           // every pred / pred_status write of the workgroup issued
+            if (threadIdx.x == 0) {
+                __threadfence();
+                atomicAdd(&a.psum_ctr[p], 1u);
+            }
+        }
     }
     FM_PROBE_AT(ts, 7);
 }
@@ -1209,11 +1135,8 @@ extern "C" int fm_ts_fused(const fm_ts_args* args, void* stream) {
     FM_REQUIRE(a.psum_mean == nullptr || (a.pred && a.psum_idx && a.psum_count && a.psum_se && a.psum_tstat &&
                                            a.psum_nobs && a.psum_ctr),
                "fm_ts_fused: the predictive summary needs pred and every psum_* buffer");
-    size_t lds = fm_ts_fused_lds_bytes(a.nseg, a.pmax, a.window, a.lag, a.roll != nullptr, a.pred != nullptr);
-    if (a.psum_mean != nullptr) {   // the last rolling workgroup stages one series per wave
-        const size_t ps = ts_ix_bytes(a.nseg) + (size_t)FNW * a.nseg * 8;
-        lds = lds > ps ? lds : ps;
-    }
+    const size_t lds = fm_ts_fused_lds_bytes(a.nseg, a.pmax, a.window, a.lag, a.roll != nullptr,
+                                             a.pred != nullptr);
     FM_REQUIRE(lds <= FM_TS_FUSED_MAX_LDS,
                "fm_ts_fused: series too long for LDS staging (use the per-stage entry points)");
     if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit: opt in (once)
@@ -1227,7 +1150,52 @@ extern "C" int fm_ts_fused(const fm_ts_args* args, void* stream) {
         }
     }
     const int nchunk = a.roll ? (a.nseg + RROWS - 1) / RROWS : 0;
-    hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk, a.nprob), dim3(FT), lds, (hipStream_t)stream, a);
+    if (a.psum_mean == nullptr) {
+        hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk, a.nprob), dim3(FT), lds, (hipStream_t)stream, a);
+        FM_CHECK_LAUNCH("fm_ts_fused");
+        return FM_OK;
+    }
+    // the predictive summary's workgroups wait on the rolling ones: only when every workgroup
+    // of the grid is resident at once; otherwise a second launch on the records, same result
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        FM_REQUIRE(hipGetDevice(&dev) == hipSuccess &&
+                       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
+                   "fm_ts_fused: cannot query the device");
+    }
+    int per_cu = 0;
+    FM_REQUIRE(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ts_fused_kernel, FT, lds) ==
+                   hipSuccess, "fm_ts_fused: occupancy query failed");
+    const int64_t grid = (int64_t)(a.kmax + nchunk + PSK) * a.nprob;
+    if (grid <= (int64_t)per_cu * cus) {
+        hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk + PSK, a.nprob), dim3(FT), lds,
+                           (hipStream_t)stream, a);
+        FM_CHECK_LAUNCH("fm_ts_fused");
+        return FM_OK;
+    }
+    fm_ts_args m = a;
+    m.psum_idx = m.psum_count = m.psum_nobs = nullptr;
+    m.psum_mean = m.psum_se = m.psum_tstat = nullptr;
+    m.psum_ctr = nullptr;
+    hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk, a.nprob), dim3(FT), lds, (hipStream_t)stream, m);
     FM_CHECK_LAUNCH("fm_ts_fused");
-    return FM_OK;
+    fm_ts_args q{};
+    q.rec = a.pred;
+    q.r_seg = 4;
+    q.r_prob = (int64_t)a.nseg * 4;
+    q.status = a.pred_status;
+    q.s_seg = 1;
+    q.s_prob = a.nseg;
+    q.nseg = a.nseg;
+    q.nprob = a.nprob;
+    q.kmax = PSK;
+    q.nw_lags = a.nw_lags;
+    q.idx = a.psum_idx;
+    q.count = a.psum_count;
+    q.mean = a.psum_mean;
+    q.se = a.psum_se;
+    q.tstat = a.psum_tstat;
+    q.nobs = a.psum_nobs;
+    return fm_ts_fused(&q, stream);
 }

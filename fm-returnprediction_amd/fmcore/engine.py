@@ -918,12 +918,6 @@ def _psum_ctr(dev, nprob):
     return _PSUM_CTR[key]
 
 
-def ts_pred_summary_fits(nseg):
-    """Whether fm_ts_fused's last rolling workgroup can stage the predictive summary (one
-    series per wave in LDS)."""
-    return ((nseg * 4 + 15) & ~15) + 4 * nseg * 8 <= L.FM_TS_FUSED_MAX_LDS
-
-
 def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_lags=4,
              window=None, min_periods=None, pmax=None, moments=None, mom_stride=0, prob_k=None,
              lag=1, seg_lo=0, seg_hi=None, predictive=False, pred_summary=False, tag="fm_ts_fused"):
@@ -932,7 +926,7 @@ def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_la
     predictive records [P, T, 4] and status [P, T].  Returns (ix, summ, roll, pred, pst);
     with ``pred_summary`` (predictive, no exchange before the summary) a sixth element, the
     predictive records' (Summary, TSIndex) -- summarize_predictive's result, bit for bit --
-    from the same launch (each problem's last rolling workgroup)."""
+    from the same launch (three more workgroups per problem wait for its rolling ones)."""
     dev = rec.device
     idx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
     cnt = torch.empty(nprob, dtype=torch.int32, device=dev)
@@ -995,14 +989,11 @@ def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag
         out = (ix, summ, roll, pred, pst)
         return out + (summarize_predictive(pred, pst, nw_lags),) if pred_summary else out
     pk = _small_tensor(tuple(p.K for p in res.problems), torch.int32, res.rec.device) if predictive else None
-    fold = pred_summary and ts_pred_summary_fits(T)
-    out = ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
-                   window=window, min_periods=min_periods,
-                   pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
-                   prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive, pred_summary=fold)
-    if pred_summary and not fold:
-        out = out + (summarize_predictive(out[3], out[4], nw_lags),)
-    return out
+    return ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
+                    window=window, min_periods=min_periods,
+                    pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
+                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive,
+                    pred_summary=pred_summary)
 
 
 def forecast(panel: DevicePanel, coef, cols=None):

@@ -66,10 +66,10 @@ class ShardedStep:
             gres = E.FMResult(problems=res.problems, rec=self.rec_g, status=self.st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
         # without an exchange of the predictive records the launch also gives their summary
-        ix, summ, roll, pred, pst, ps = LW.time_series_stage(gres, self.cfg, moments=res.moments,
-                                                             seg_lo=self.seg_lo, seg_hi=self.seg_hi,
-                                                             pred_summary=not self.exchange)
-        self._psum = ps
+        out = LW.time_series_stage(gres, self.cfg, moments=res.moments, seg_lo=self.seg_lo,
+                                   seg_hi=self.seg_hi, pred_summary=not self.exchange)
+        ix, summ, roll, pred, pst = out[:5]
+        self._psum = out[5] if len(out) > 5 else None
         return gres, summ, pred, pst
 
     def exchange_pred(self, pred, pst):

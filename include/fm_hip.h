@@ -360,10 +360,12 @@ typedef struct fm_ts_args {
     double* pred;                 /* [nprob][nseg][4] or NULL */
     uint32_t* pred_status;        /* [nprob][nseg] */
     /* The predictive records' FM summary inside this launch (runs with no exchange between
-     * the two stages): with psum_mean set (pred set too), the last rolling workgroup of each
-     * problem compacts its pred_status and summarizes the first 3 fields of its pred records
-     * -- what fm_ts_fused on (pred, 4, nseg*4, pred_status, 1, nseg, nseg, nprob, kmax 3)
-     * returns, bit for bit.  All NULL (zero-initialised): no predictive summary here. */
+     * the two stages): with psum_mean set (pred set too), three more workgroups per problem
+     * wait until the problem's rolling workgroups are done, then compact its pred_status and
+     * summarize the first 3 fields of its pred records -- what fm_ts_fused on (pred, 4,
+     * nseg*4, pred_status, 1, nseg, nseg, nprob, kmax 3) returns, bit for bit.  When the grid
+     * would not be resident at once, a second launch does exactly that.  All NULL
+     * (zero-initialised): no predictive summary here. */
     int32_t* psum_idx;            /* [nprob][nseg] */
     int32_t* psum_count;          /* [nprob] */
     double* psum_mean;            /* [nprob][3] */

@@ -1202,8 +1202,8 @@ def test_pipeline_headline_panel_full_size(E):
 
 
 def test_pred_summary_in_launch_bit_identical(E):
-    """The predictive records' FM summary computed by fm_ts_fused's last rolling workgroup of
-    each problem (world-1 runs, psum_*) equals the separate fm_ts_fused launch on the records
+    """The predictive records' FM summary computed inside fm_ts_fused (world-1 runs, psum_*:
+    three workgroups per problem wait for its rolling workgroups) equals the separate fm_ts_fused launch on the records
     (summarize_predictive) bit for bit: means, NW standard errors, t-stats, counts and the
     compacted month index; repeated launches (the arrival counters reset themselves), a
     problem with no fitted month, and a series with unfitted months inside."""
@@ -1217,7 +1217,6 @@ def test_pred_summary_in_launch_bit_identical(E):
     st[7:11, 2] = 0              # unfitted months inside problem 2's series
     g = E.FMResult(problems=res.problems, rec=res.rec, status=st, pmax=res.pmax, moments=res.moments,
                    mom_stride=res.mom_stride)
-    assert E.ts_pred_summary_fits(g.rec.shape[0])
     for _ in range(3):
         ix, summ, roll, pred, pst, ps = LW.time_series_stage(g, cfg, moments=res.moments, pred_summary=True)
         psumm, pix = ps

@@ -32,6 +32,7 @@ for s in "$@"; do
                      "pmcw:::300:::$PROF --pmc WRITE_SIZE -d $R/gpurun_out/pmcw -o w --output-format csv -- python3 $R/tools/pmc_run.py");;
     sq)      specs+=("sqa$SQ_TAG:::120:::$PROF --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU -d $R/gpurun_out/sqa$SQ_TAG -o s --output-format csv -- python3 $R/tools/pmc_run.py"
                      "sqb$SQ_TAG:::120:::$PROF --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES -d $R/gpurun_out/sqb$SQ_TAG -o s --output-format csv -- python3 $R/tools/pmc_run.py");;
+    icache)  specs+=("icache$SQ_TAG:::120:::$PROF --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU -d $R/gpurun_out/icache$SQ_TAG -o s --output-format csv -- python3 $R/tools/pmc_run.py");;
     *) echo "unknown step $s"; exit 2;;
   esac
 done
@@ -41,6 +42,9 @@ if [ -f gpurun_out/sqa$SQ_TAG/s_counter_collection.csv ]; then
   for p in sqa$SQ_TAG sqb$SQ_TAG; do
     python tools/pmc_summary.py gpurun_out/$p/s_counter_collection.csv ${SQ_KERNELS:-universe_kernel gram_kernel select_pair select_fixup solve16 ts_fused} > gpurun_out/$p.summary 2>&1
   done
+fi
+if [ -f gpurun_out/icache$SQ_TAG/s_counter_collection.csv ]; then
+  python tools/pmc_summary.py gpurun_out/icache$SQ_TAG/s_counter_collection.csv ${SQ_KERNELS:-universe_kernel gram_kernel select_pair select_fixup solve16 ts_fused} > gpurun_out/icache$SQ_TAG.summary 2>&1
 fi
 if [ -f gpurun_out/pmcf/f_counter_collection.csv ] && [ -f gpurun_out/pmcw/w_counter_collection.csv ]; then
   sha=$(python -c "import hashlib;print(hashlib.sha256(open('fm-returnprediction_amd/lib/libfm_hip.so','rb').read()).hexdigest()[:16])")

@@ -21,9 +21,11 @@ from fmcore import lewellen as LW  # noqa: E402
 SLOTS = 8
 # tag -> (probe buffer, slot names)
 TAGS = {
-    "fm_universe": ("sel", {0: "start", 1: "loaded+reduced", 2: "hist_select", 3: "levels"}),
+    "fm_universe": ("sel", {0: "start", 1: "loaded+reduced", 4: "hs: histogram", 5: "hs: scan+locate",
+                            6: "hs: lists", 7: "hs: sorted", 2: "hist_select", 3: "levels"}),
     "fm_select_cuts": ("sel", {4: "fixup start", 5: "fixup read nwork"}),
-    "fm_solve": ("solve", {0: "start", 1: "partials", 2: "cumulative", 3: "problems"}),
+    "fm_solve": ("solve", {0: "start", 1: "partials", 2: "cumulative", 4: "w0 gram rows", 5: "w0 centered",
+                           6: "w0 cholesky", 7: "w0 back-subst", 3: "problems"}),
     "fm_solve_fixup": ("solve", {4: "start", 5: "end"}),
     "fm_ts_fused": ("ts", {0: "start", 1: "compact", 2: "gather", 3: "dropna|prefix", 4: "nw|rolled",
                            5: "pred preload", 6: "rolling done", 7: "end (+pred summary)"}),
@@ -54,7 +56,7 @@ def probe(tag, buf, names):
     host = (ctypes.c_uint32 * (SLOTS * n))()
     assert getattr(lib, f"fm_probe_copy_{buf}")(host, n) == 0
     f = np.frombuffer(host, dtype=np.uint32).reshape(n, SLOTS).astype(np.int64)
-    slots = sorted(names)
+    slots = list(names)   # in the listed (execution) order
     live = (f[:, slots[0]] != 0)
     f = f[live]
     if f.shape[0] == 0:
