@@ -65,9 +65,10 @@ class ShardedStep:
         if self.exchange:
             gres = E.FMResult(problems=res.problems, rec=self.rec_g, status=self.st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
-        # without an exchange of the predictive records the launch also gives their summary
+        # without an exchange of the predictive records the launch can also give their summary
+        # (PRED_SUMMARY_IN_LAUNCH; measured slower than its own launch, so off)
         out = LW.time_series_stage(gres, self.cfg, moments=res.moments, seg_lo=self.seg_lo,
-                                   seg_hi=self.seg_hi, pred_summary=not self.exchange)
+                                   seg_hi=self.seg_hi, pred_summary=LW.PRED_SUMMARY_IN_LAUNCH and not self.exchange)
         ix, summ, roll, pred, pst = out[:5]
         self._psum = out[5] if len(out) > 5 else None
         return gres, summ, pred, pst
