@@ -84,19 +84,17 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     };
     int c1 = 0, c0 = 0;
     if (a.queue != nullptr) {
-        // dynamic plan: chunks from the queue; the next grab is in flight during each chunk
+        // dynamic plan: workgroup b takes queue position b first (no atomic: 768 same-address
+        // atomics at launch serialize for tens of microseconds), then positions nwg + (a grab
+        // of the queue counter) as it finishes, so the grabs spread out in time
         __shared__ int qnext;
-        if (tid == 0) qnext = atomicAdd(&a.queue[0], 1);
-        __syncthreads();
-        int q = qnext;
+        int q = (int)blockIdx.x;
         bool first = true;
         while (q < a.nchunks) {   // block-uniform
-            int qn = 0;
-            if (tid == 0) qn = atomicAdd(&a.queue[0], 1);
             chunk_body(a.chunk_order ? a.chunk_order[q] : a.nchunks - 1 - q, first);
             first = false;
             ++c1;
-            if (tid == 0) qnext = qn;   // every thread read the last value before the chunk's barriers
+            if (tid == 0) qnext = (int)gridDim.x + atomicAdd(&a.queue[0], 1);
             __syncthreads();
             q = qnext;
         }
