@@ -146,8 +146,8 @@ constexpr int ST_R = FM_STD_R;       // consecutive rows per thread
 constexpr int ST_ROWS = ST_T * ST_R; // rows per tile
 constexpr int ST_HA = 128;           // halo rows are loaded from a 128-row aligned start
 #ifndef FM_STD_LP
-#define FM_STD_LP 4                  // load batches per thread (5: 105 VGPRs, one wave per SIMD less)
-#endif
+#define FM_STD_LP 2                  // load batches per thread in flight: 2 -> 74 VGPRs, 0.1034 ms;
+#endif                               // 3 -> 74, 0.1064; 4 -> 88, 0.1116 (profiles/r05/v4_stdbench_lp.log)
 
 // LDS slot of halo element e: one pad slot per ST_R (the lanes of a wave read elements
 // ST_R apart; stride ST_R + 1 doubles puts 32 lanes on distinct bank pairs)
