@@ -219,9 +219,11 @@ __device__ __forceinline__ void zero_sign_unit(const SelArgs& a, int s, int c, A
     }
 }
 
+// The fix-up work of workgroup `bid` of `nblk` (the fix-up launch, or the fix-up part of
+// the launch it shares with the universe)
 template <int VPT>   // VPT == 0: the streaming exact path
-__global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs, int zs_len) {
-    __shared__ FixSmem sm;
+__device__ __forceinline__ void fixup_body(const SelArgs& a, double* zs, int zs_len, uint32_t bid, uint32_t nblk,
+                                           FixSmem& sm) {
     SelCtl* ctl = a.ctl;
     SelArgs b = a;
     b.ctl = nullptr;
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs,
     // more than the whole no-op launch)
     FM_PROBE_AT(sel, 5);
     if (nw == 0) return;
-    for (uint32_t i = blockIdx.x; i < nw; i += gridDim.x) {
+    for (uint32_t i = bid; i < nw; i += nblk) {
         const uint32_t u = ctl->work[i];
         const int s = (int)(u % (uint32_t)b.nseg), c = (int)(u / (uint32_t)b.nseg);
         if constexpr (VPT > 0) select_unit_wg<VPT>(b, s, c, sm.sel);
@@ -242,7 +244,7 @@ __global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs,
         if (b.lerp_mode == 0 && threadIdx.x < WAVE) {
             const int64_t L = b.seg_off[s + 1] - b.seg_off[s];
             if (L <= ZS_LDS) zero_sign_unit(b, s, c, NpLds{sm.arr});
-            else zero_sign_unit(b, s, c, NpGlobal{zs + (int64_t)blockIdx.x * zs_len});
+            else zero_sign_unit(b, s, c, NpGlobal{zs + (int64_t)bid * zs_len});
         }
         __threadfence();
         __syncthreads();
@@ -250,11 +252,39 @@ __global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs,
     if (threadIdx.x == 0) {
         __threadfence();
         const uint32_t t = atomicAdd(&ctl->done, 1u);
-        if (t == gridDim.x - 1) {
+        if (t == nblk - 1) {
             __hip_atomic_store(&ctl->nwork, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+template <int VPT>
+__global__ __launch_bounds__(ST) void select_fixup_kernel(SelArgs a, double* zs, int zs_len) {
+    __shared__ FixSmem sm;
+    fixup_body<VPT>(a, zs, zs_len, blockIdx.x, gridDim.x, sm);
+}
+
+template <int VPT>
+__device__ __forceinline__ void universe_month(const double* __restrict__ me, const uint8_t* __restrict__ nyse,
+                                               const int64_t* __restrict__ seg_off, double qa, double qb,
+                                               double* __restrict__ cut_a, double* __restrict__ cut_b,
+                                               uint8_t* __restrict__ level, int s, SelSmem& sm);
+
+// The select fix-up and get_subsets' NYSE breakpoints + level bytes in ONE launch (the two
+// are independent; the universe no longer needs a launch of its own before the select):
+// workgroups [0, nseg) are universe_kernel's months, the rest the fix-up's workgroups (which
+// return at once when no unit is marked).  Held to universe_kernel's 3 waves per SIMD.
+template <int VPT>
+__global__ __launch_bounds__(ST, 3) void select_fixup_universe_kernel(SelArgs a, double* zs, int zs_len) {
+    __shared__ FixSmem sm;
+    const int nuni = a.nseg;
+    if ((int)blockIdx.x < nuni) {   // block-uniform
+        universe_month<VPT>(a.ume, a.unyse, a.seg_off, a.uq_a, a.uq_b, a.ucut_a, a.ucut_b, a.ulevel, (int)blockIdx.x,
+                            sm.sel);
+        return;
+    }
+    fixup_body<VPT>(a, zs, zs_len, blockIdx.x - nuni, gridDim.x - nuni, sm);
 }
 
 int64_t ws_list_bytes(int64_t nunits) { return ((int64_t)offsetof(SelCtl, work) + 4 * nunits + 255) / 256 * 256; }
@@ -280,6 +310,26 @@ void launch_fixup(const SelArgs& a, int max_seg_len, hipStream_t st) {
     else if (vpt <= 20) hipLaunchKernelGGL(select_fixup_kernel<20>, dim3(g), dim3(ST), 0, st, a, zs, zl);
     else if (vpt <= FM_SELECT_STREAM_VPT) hipLaunchKernelGGL(select_fixup_kernel<FM_SELECT_STREAM_VPT>, dim3(g), dim3(ST), 0, st, a, zs, zl);
     else hipLaunchKernelGGL(select_fixup_kernel<0>, dim3(g), dim3(ST), 0, st, a, zs, zl);
+}
+
+// fix-up + universe in one launch (months of <= 20 x 256 rows): the fix-up workgroups are
+// the slots the universe's months leave in one resident round (3 per CU), at least 32
+int launch_fixup_universe(const SelArgs& a, int max_seg_len, hipStream_t st) {
+    static int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int vpt = (max_seg_len + ST - 1) / ST;
+    int nfix = 3 * ncu - a.nseg;
+    nfix = nfix < 32 ? 32 : (nfix > fix_grid(max_seg_len) ? fix_grid(max_seg_len) : nfix);
+    double* zs = (double*)((char*)a.ctl + ws_list_bytes((int64_t)a.nseg * a.ncols));
+    const dim3 g((unsigned)(a.nseg + nfix));
+    if (vpt <= 8) hipLaunchKernelGGL(select_fixup_universe_kernel<8>, g, dim3(ST), 0, st, a, zs, max_seg_len);
+    else hipLaunchKernelGGL(select_fixup_universe_kernel<20>, g, dim3(ST), 0, st, a, zs, max_seg_len);
+    return FM_OK;
 }
 
 // One unit per workgroup (grid nseg x ncols).
@@ -1802,20 +1852,20 @@ void launch_select_wave(const SelArgs& a, hipStream_t st) {
 // finds the pandas groupby.quantile(q_a, q_b) order statistics of the NYSE rows (NaN me
 // skipped) by the adaptive histogram select, lerps them the pandas way, and writes every
 // row's level (me >= me_20) + (me >= me_50) from the same registers (NaN compares False).
+#ifndef FM_AB_UNI_APART
+#define FM_AB_UNI_APART 0   // timing builds only: the universe in its own launch before the select
+#endif
 #ifndef FM_AB_UNI_NOSELECT
 #define FM_AB_UNI_NOSELECT 0   // timing builds only (tools/build_variant.sh): skip the order statistics
 #endif
 template <int VPT>
-__global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const double* __restrict__ me,
-                                                      const uint8_t* __restrict__ nyse,
-                                                      const int64_t* __restrict__ seg_off, double qa,
-                                                      double qb, double* __restrict__ cut_a,
-                                                      double* __restrict__ cut_b,
-                                                      uint8_t* __restrict__ level) {
+__device__ __forceinline__ void universe_month(const double* __restrict__ me, const uint8_t* __restrict__ nyse,
+                                               const int64_t* __restrict__ seg_off, double qa, double qb,
+                                               double* __restrict__ cut_a, double* __restrict__ cut_b,
+                                               uint8_t* __restrict__ level, int s, SelSmem& sm) {
     static_assert(VPT <= 64, "universe_kernel: NYSE flags are one 64-bit mask per thread");
-    __shared__ SelSmem sm;
     FM_PROBE_AT(sel, 0);
-    const int s = blockIdx.x, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const int64_t r0 = seg_off[s];
     const int L = (int)(seg_off[s + 1] - r0);
     const int last = L > 0 ? L - 1 : 0;
@@ -1894,6 +1944,17 @@ __global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const d
         if (idx < L) level[r0 + idx] = (uint8_t)((xm[v] >= a ? 1 : 0) + (xm[v] >= b ? 1 : 0));
     }
     FM_PROBE_AT(sel, 3);
+}
+
+template <int VPT>
+__global__ __launch_bounds__(ST, VPT <= 20 ? 3 : 1) void universe_kernel(const double* __restrict__ me,
+                                                      const uint8_t* __restrict__ nyse,
+                                                      const int64_t* __restrict__ seg_off, double qa,
+                                                      double qb, double* __restrict__ cut_a,
+                                                      double* __restrict__ cut_b,
+                                                      uint8_t* __restrict__ level) {
+    __shared__ SelSmem sm;
+    universe_month<VPT>(me, nyse, seg_off, qa, qb, cut_a, cut_b, level, (int)blockIdx.x, sm);
 }
 
 }  // namespace
@@ -2024,7 +2085,10 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
     // 118 vs 83 + 23 us on the bench panel, profiles/r04/v2_kbench_fused_universe.log)
     const bool ride = u != nullptr && long_path && !long_is_mid(a, max_seg_len) &&
                       (FM_HK_RIDE || FM_AB_LONG_F64 || FM_AB_LONG != 0);
-    if (u != nullptr && !ride) {
+    // months of <= 20 x 256 rows on the register paths: the universe shares the fix-up's launch
+    // after the select (one launch less; the two are independent)
+    const bool with_fixup = u != nullptr && !ride && !long_path && vpt <= 20 && !FM_AB_UNI_APART;
+    if (u != nullptr && !ride && !with_fixup) {
         const int rcu = universe_separately(x, u, stream);
         if (rcu != FM_OK) return rcu;
     }
@@ -2085,7 +2149,13 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
         else launch_select<FM_SELECT_STREAM_VPT>(a, ncols, st);
         FM_CHECK_LAUNCH("fm_select_cuts");
     }
-    launch_fixup(a, max_seg_len, st);
+    if (with_fixup) {
+        SelArgs au = a;
+        set_universe(au, u);
+        launch_fixup_universe(au, max_seg_len, st);
+    } else {
+        launch_fixup(a, max_seg_len, st);
+    }
     FM_CHECK_LAUNCH("fm_select_cuts(fix-up)");
     return a.level ? fm_universe_level(cols, seg_off, nseg, (int64_t)max_seg_len * nseg, x.lo, x.hi, x.level, stream) : FM_OK;
 }

@@ -128,13 +128,11 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
     nlevels = 1
     models, names = build_models(panel, model_cols, y=y, fig1=cfg.fig1, universes=cfg.universes)
     select = cfg.winsorize or cfg.standardize
-    # long months (C5's 20,000 firms: fm_select's long-month kernel) put the universe months
-    # into the winsorize launch (fm_select_universe: one more grid column); short ones keep
-    # fm_universe's own launch, on the pass's own stream (riding the two-wave kernel measured
-    # slower, and a side-stream fork / join inside the captured graph cost more in cross-queue
-    # synchronization than the overlap saved)
-    fused_universe = (cfg.universes and select and not cfg.standardize and
-                      E.SELECT_LONG_MIN < panel.max_seg_len <= E.SELECT_LONG_MAX)
+    # get_subsets' NYSE breakpoints + level bytes come with the winsorize call
+    # (fm_select_universe): on the bench's short months they share the select fix-up's launch
+    # (the universe no longer needs a launch of its own), on C5's long months they ride the
+    # long-month kernel's launch (one more grid column); other paths launch fm_universe first
+    fused_universe = cfg.universes and select and not cfg.standardize
     if cfg.universes and not fused_universe:
         a, b, level = E.universe(panel)
         nlevels = 3
