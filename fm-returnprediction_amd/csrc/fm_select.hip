@@ -1993,10 +1993,11 @@ extern "C" int64_t fm_select_ws_bytes(int32_t nseg, int32_t ncols, int32_t max_s
 
 namespace fm {
 namespace {
-// fm_select, optionally with get_subsets' NYSE breakpoints + level bytes (u != NULL): they ride
-// the long-month high-key kernel's launch (6,145 .. 20,480-row months, tail ranks, no row mask:
-// one more grid column); on every other path, including the two-wave and MID kernels, the
-// universe is launched on its own first (fm_universe, or the row-masked select), same outputs.
+// fm_select, optionally with get_subsets' NYSE breakpoints + level bytes (u != NULL): months of
+// <= 5,120 rows on the register paths share the select fix-up's launch after the select; they
+// ride the long-month high-key kernel's launch (6,145 .. 20,480-row months, tail ranks, no row
+// mask: one more grid column); on the other paths (MID, streaming) the universe is launched
+// on its own first (fm_universe, or the row-masked select), same outputs.
 int select_impl(const fm_select_args* args, const fm_universe_args* u, void* stream);
 }  // namespace
 }  // namespace fm
@@ -2080,9 +2081,9 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
     const bool long_path = vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && x.mean == nullptr &&
                            nvalid != nullptr && !FM_AB_SELECT_STREAM;
     // a universe rides the long-month kernel's launch (one more grid column) unless its tails
-    // need the histogram (MID) kernel; on every other path it is launched first, on its own
-    // (riding the two-wave kernel's persistent workgroups measured slower for short months:
-    // 118 vs 83 + 23 us on the bench panel, profiles/r04/v2_kbench_fused_universe.log)
+    // need the histogram (MID) kernel (riding the two-wave kernel's persistent workgroups
+    // measured slower for short months: 118 vs 83 + 23 us on the bench panel,
+    // profiles/r04/v2_kbench_fused_universe.log)
     const bool ride = u != nullptr && long_path && !long_is_mid(a, max_seg_len) &&
                       (FM_HK_RIDE || FM_AB_LONG_F64 || FM_AB_LONG != 0);
     // months of <= 20 x 256 rows on the register paths: the universe shares the fix-up's launch

@@ -70,7 +70,8 @@ struct SelArgs {
     double* prm;   // optional LDS [3][32]: thread 0 also stores lo, hi, center of column c there
     uint8_t* level;   // fm_select_args.level (written by fm_universe_level after the cuts)
     // fm_select_universe: get_subsets' NYSE breakpoints + level bytes of every month, done by
-    // one more grid column of the long-month high-key kernel (ume == NULL: none)
+    // one more grid column of the long-month high-key kernel or by the first nseg workgroups
+    // of the select fix-up's launch (ume == NULL: none)
     const double* ume = nullptr;
     const uint8_t* unyse = nullptr;
     double uq_a = 0.0, uq_b = 0.0;

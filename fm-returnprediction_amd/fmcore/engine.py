@@ -268,9 +268,10 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
     also the clipped mean / sd; ``center``: also a Gram pivot inside the data; ``level``
     (uint8 [rows], one column): every row's (x >= lo) + (x >= hi) (fm_select).
     ``universe`` = (q_a, q_b): also get_subsets' NYSE breakpoints and level bytes of the
-    panel's me / nyse rows in the same call (fm_select_universe: riding the long-month
-    kernel's launch for 6,145-20,480-row months without the histogram (MID) variant, its own
-    launch otherwise); returns (Cuts, (cut_a, cut_b, level)) then."""
+    panel's me / nyse rows in the same call (fm_select_universe: sharing the select fix-up's
+    launch for months of <= 5,120 rows, riding the long-month kernel's launch for
+    6,145-20,480-row months without the histogram (MID) variant, its own launch first
+    otherwise); returns (Cuts, (cut_a, cut_b, level)) then."""
     src = panel.cols if cols is None else cols
     if src.dim() == 1:
         src = src.view(1, -1)

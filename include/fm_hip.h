@@ -255,10 +255,11 @@ int fm_select(const fm_select_args* args, void* stream);
  * bytes (get_subsets, reference src/calc_Lewellen_2014.py:69-105) over the same month
  * segments (args->seg_off / nseg / max_seg_len), written to cut_a / cut_b [nseg] and level
  * [rows]: the winsorize cuts of calc_Lewellen_2014.py:516-527 and the universes of :74-96 in
- * one call.  Months of 6,145 .. 20,480 rows (fm_select's long-month path, no row mask, no
- * moments) put the universe months into the same launch (one more grid column); otherwise
- * the universe runs first, on its own (fm_universe, or the row-masked select + level bytes
- * past 16,384 rows).  Outputs are identical to fm_select + fm_universe. */
+ * one call.  Months of <= 5,120 rows (the register select paths) run the universe months in
+ * the select fix-up's launch; months of 6,145 .. 20,480 rows (fm_select's long-month path,
+ * no row mask, no moments) put them into the long-month launch (one more grid column);
+ * otherwise the universe runs first, on its own (fm_universe, or the row-masked select +
+ * level bytes past 16,384 rows).  Outputs are identical to fm_select + fm_universe. */
 typedef struct fm_universe_args {
     const double* me;            /* [rows] */
     const uint8_t* nyse;         /* [rows] nonzero = NYSE row */

@@ -472,13 +472,13 @@ def test_universe_kernel_vs_oracle(E):
         assert np.array_equal(level[off[t]:off[t + 1]], exp), t
 
 
-@pytest.mark.parametrize("maxlen", [6144, 9000, 20000, 24000])
+@pytest.mark.parametrize("maxlen", [2500, 5120, 6144, 9000, 20000, 24000])
 def test_select_universe_fused(E, maxlen):
     """fm_select_universe: the winsorize cuts and get_subsets' NYSE breakpoints + level bytes
-    from one call.  Months of 6,145-20,480 rows ride the long-month high-key kernel's launch
-    (one more grid column); shorter months (the two-wave kernel) and longer ones (the
-    streaming select) launch the universe on its own first (fm_universe / the row-masked NYSE
-    select).  Cuts must equal fm_select's alone bit for bit, breakpoints the
+    from one call.  Months of <= 5,120 rows (the two-wave kernel) run the universe in the
+    select fix-up's launch; 6,145-20,480 rows ride the long-month high-key kernel's launch
+    (one more grid column); 5,121-6,144 (the workgroup kernel) and longer ones (the streaming
+    select) launch the universe on its own first (fm_universe / the row-masked NYSE select).  Cuts must equal fm_select's alone bit for bit, breakpoints the
     pandas lerp restatement and levels the reference's masks, over adversarial me months
     (clusters, ties, NaN me, no NYSE row, every NYSE me NaN, 1-row months)."""
     rng = np.random.default_rng(77)
