@@ -53,9 +53,22 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 #if FM_GRAM_WGTIME
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
+    // default order last-first: fm_select streams the panel month by month, so the months it
+    // read last are still in the memory-side cache when they are read here; with a
+    // chunk_order (the split-month plan) the big chunks go first, the small ones fill in; with
+    // a balanced plan (wg_chunk_off) workgroup b takes its run of consecutive chunks
+    int c0, c1;
+    if (a.wg_chunk_off != nullptr) {
+        const int b = (int)gridDim.x - 1 - (int)blockIdx.x;
+        c0 = a.wg_chunk_off[b];
+        c1 = a.wg_chunk_off[b + 1];
+    } else {
+        c0 = a.chunk_order ? a.chunk_order[blockIdx.x] : (int)gridDim.x - 1 - (int)blockIdx.x;
+        c1 = c0 + 1;
+    }
     const int npat = 1 << a.nmodels;
     const int lutv = a.pattern_id[tid < npat ? tid : 0];
-    auto chunk_body = [&](int chunk, bool first) {
+    for (int chunk = c0; chunk < c1; ++chunk) {
         const int seg = a.chunk_seg[chunk];
         const int64_t r0 = a.chunk_row[2 * chunk], r1 = a.chunk_row[2 * chunk + 1];
         // Prologue loads (month parameters) are unconditional (pointer/index selected, value
@@ -73,7 +86,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         }
         GramWave<NT, NB, GNW, PL> g(a, r0, r1, w);
         g.prefetch();
-        if (first) {
+        if (chunk == c0) {
             for (int e = tid; e < 4 * S::RS; e += GT) zblk[e] = 0.0;
             if (tid < 64) lut[tid] = (uint8_t)lutv;
         }
@@ -81,45 +94,6 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
         __syncthreads();
         g.run(prm, lut, a.inv_scale != nullptr, tile, zblk);
         g.epilogue(tile, a.partial + (int64_t)chunk * nbr * S::PK, nbr);
-    };
-    int c1 = 0, c0 = 0;
-    if (a.queue != nullptr) {
-        // dynamic plan: workgroup b takes queue position b first (no atomic: 768 same-address
-        // atomics at launch serialize for tens of microseconds), then positions nwg + (a grab
-        // of the queue counter) as it finishes, so the grabs spread out in time
-        __shared__ int qnext;
-        int q = (int)blockIdx.x;
-        bool first = true;
-        while (q < a.nchunks) {   // block-uniform
-            chunk_body(a.chunk_order ? a.chunk_order[q] : a.nchunks - 1 - q, first);
-            first = false;
-            ++c1;
-            if (tid == 0) qnext = (int)gridDim.x + atomicAdd(&a.queue[0], 1);
-            __syncthreads();
-            q = qnext;
-        }
-        if (tid == 0) {   // the last workgroup out resets the queue for the next launch
-            __threadfence();
-            const int t = atomicAdd(&a.queue[1], 1);
-            if (t == (int)gridDim.x - 1) {
-                __hip_atomic_store(&a.queue[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&a.queue[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    } else {
-        // default order last-first: fm_select streams the panel month by month, so the months
-        // it read last are still in the memory-side cache when they are read here; with a
-        // chunk_order (the split-month plan) the big chunks go first, the small ones fill in;
-        // with a balanced plan (wg_chunk_off) workgroup b takes its run of consecutive chunks
-        if (a.wg_chunk_off != nullptr) {
-            const int b = (int)gridDim.x - 1 - (int)blockIdx.x;
-            c0 = a.wg_chunk_off[b];
-            c1 = a.wg_chunk_off[b + 1];
-        } else {
-            c0 = a.chunk_order ? a.chunk_order[blockIdx.x] : (int)gridDim.x - 1 - (int)blockIdx.x;
-            c1 = c0 + 1;
-        }
-        for (int chunk = c0; chunk < c1; ++chunk) chunk_body(chunk, chunk == c0);
     }
 #if FM_GRAM_WGTIME
     if (tid == 0 && blockIdx.x < WGT_MAX) {
@@ -135,7 +109,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 
 template <int NT, int NB, int MINW>
 void launch_gram(const fm_gram_args& a, hipStream_t st) {
-    const int grid = (a.wg_chunk_off != nullptr || a.queue != nullptr) ? a.nwg : a.nchunks;
+    const int grid = a.wg_chunk_off != nullptr ? a.nwg : a.nchunks;
     if (a.hi_plane != nullptr)
         hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true>), dim3(grid), dim3(GT), 0, st, a);
     else
@@ -168,9 +142,8 @@ extern "C" int fm_gram(const fm_gram_args* args, void* stream) {
                FM_MAX_LEVELS);
     FM_REQUIRE(a.npatterns >= 1, "fm_gram: npatterns must be >= 1");
     if (a.nchunks == 0) return FM_OK;
-    FM_REQUIRE(a.wg_chunk_off == nullptr || (a.nwg >= 1 && a.chunk_order == nullptr && a.queue == nullptr),
-               "fm_gram: a balanced plan needs nwg >= 1, no chunk_order and no queue");
-    FM_REQUIRE(a.queue == nullptr || a.nwg >= 1, "fm_gram: a dynamic plan needs nwg >= 1");
+    FM_REQUIRE(a.wg_chunk_off == nullptr || (a.nwg >= 1 && a.chunk_order == nullptr),
+               "fm_gram: a balanced plan needs nwg >= 1 and no chunk_order");
     const int nb = a.npatterns * a.nlevels;
     hipStream_t st = (hipStream_t)stream;
     if (a.ncols <= 15) {

@@ -43,7 +43,7 @@ class GramArgs(C.Structure):
         ("pattern_id", _p), ("npatterns", _i32),
         ("partial", _p), ("flags", _p), ("chunk_order", _p),
         ("hi_plane", _p), ("lo_plane", _p), ("plane_stride", _i64),
-        ("wg_chunk_off", _p), ("nwg", _i32), ("queue", _p),
+        ("wg_chunk_off", _p), ("nwg", _i32),
     ]
 
 

@@ -596,7 +596,6 @@ class _Plan:
     order: Optional[torch.Tensor] = None   # fm_gram launch order (split plan) or None
     wg_off: Optional[torch.Tensor] = None  # balanced plan: each workgroup's chunk range
     nwg: int = 0
-    queue: Optional[torch.Tensor] = None   # dynamic plan: [2] zeroed chunk-queue counters
 
 
 def _chunk_plan(panel: DevicePanel):
@@ -612,20 +611,15 @@ def _chunk_plan(panel: DevicePanel):
     if pol is None and not split:
         pol = chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len)
     order = wg = None
-    nwg, queue = 0, None
-    dev = panel.cols.device
     if split:
         seg, rows, off, order = make_chunks_split(panel.seg_off_h)
     elif pol[0] == "balanced":
         seg, rows, off, wg = make_chunks_balanced(panel.seg_off_h, pol[1], panel.row_origin)
-        nwg = len(wg) - 1
     else:
         seg, rows, off = make_chunks(panel.seg_off_h, pol[1])
-        if pol[0] == "dynamic":   # the chunks of the months plan, taken from a queue
-            nwg = min(len(seg), _num_cus() * GRAM_SLOTS_PER_CU)
-            queue = torch.zeros(2, dtype=torch.int32, device=dev)
+    dev = panel.cols.device
     t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    plan = _Plan(t(seg), t(rows), t(off), len(seg), t(order), t(wg), nwg, queue)
+    plan = _Plan(t(seg), t(rows), t(off), len(seg), t(order), t(wg), 0 if wg is None else len(wg) - 1)
     panel._chunk_cache = plan
     return plan
 
@@ -778,7 +772,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
             model_ymask=gpl.ym.data_ptr(), nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(),
             npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr(),
             chunk_order=_ptr(plan.order), hi_plane=ph, lo_plane=pl_, plane_stride=pst,
-            wg_chunk_off=_ptr(plan.wg_off), nwg=plan.nwg, queue=_ptr(plan.queue))
+            wg_chunk_off=_ptr(plan.wg_off), nwg=plan.nwg)
         _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
         _remember("fm_gram", "fm_gram", ga, src, partial, flags, lo, hi, shift, inv_scale, level, plan, gpl)
         grec, gst, gmom = _solve_group(panel, src, gpl, partial, plan.seg_chunk_off, zw, nlevels, T, pmax,

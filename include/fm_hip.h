@@ -134,12 +134,6 @@ typedef struct fm_gram_args {
      * every workgroup gets the same number of rows).  NULL: one chunk per workgroup */
     const int32_t* wg_chunk_off;
     int32_t nwg;
-    /* optional dynamic plan: nwg workgroups take chunks from a queue -- chunk chunk_order[q]
-     * (or nchunks-1-q) for q = atomicAdd(&queue[0], 1) -- until q reaches nchunks, so a
-     * workgroup that runs fast takes more chunks; the last workgroup to finish resets
-     * queue[0..1] to zero.  queue: [2] counters, zero before the first launch.  Each chunk's
-     * partial is the same whichever workgroup takes it.  NULL: static plans above */
-    int32_t* queue;
 } fm_gram_args;
 /* The argument structs (fm_gram_args, fm_solve_args, fm_select_args, ...) grow at the end:
  * zero-initialize them before filling fields, so fields a caller does not know are NULL / 0. */

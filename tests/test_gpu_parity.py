@@ -1013,7 +1013,7 @@ def test_rolling_skips_infinite_coefficients(CL):
     assert np.isfinite(got.values[75:]).all()
 
 
-@pytest.mark.parametrize("policy", ["default", "balanced", "dynamic"])
+@pytest.mark.parametrize("policy", ["default", "balanced"])
 def test_sharded_pipeline_bit_identical(E, policy):
     """SURVEY §8(e) on one GPU: split a ragged panel into 3 month ranges with
     dist.shard_bounds, run local_stage per range with the GLOBAL chunk policy (whole-month
@@ -1027,8 +1027,7 @@ def test_sharded_pipeline_bit_identical(E, policy):
     _unfitted_early_months(a)
     cols = list(dict.fromkeys(["retx"] + [c for xs in LW.table2_models().values() for c in xs] + LW.FIG1_VARS))
     panel = E.panel_from_arrays([a[c] for c in cols], cols, a["month"], me=a["me"], nyse=a["nyse"])
-    pol = {"default": E.chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len), "balanced": ("balanced", 997),
-           "dynamic": ("dynamic", 150)}[policy]
+    pol = {"default": E.chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len), "balanced": ("balanced", 997)}[policy]
     panel.chunk_policy = pol
     cfg = LW.PipelineConfig()
     mc = LW.table2_models()
@@ -1594,32 +1593,23 @@ def test_rolling_mean_outlier_months(E, fused):
 def test_split_month_gram_plan_matches_whole(E):
     """The split-month Gram plan (each month as a 3/4 + 1/4 chunk pair, big chunks launched
     first) and the balanced plan (workgroups of equal row counts cut at month boundaries,
-    workgroups spanning two months) and the dynamic plan (quarter-month chunks taken from a
-    queue: bit-identical to the same chunks launched one per workgroup) against whole-month
-    chunks on the same 600-month panel:
+    workgroups spanning two months) against whole-month chunks on the same 600-month panel:
     identical month lists, N and status; params and R2 within 1e-12 of the series scale (only
     the summation order differs)."""
     from fmcore import lewellen as LW
     panel = E.panel_synthetic(600, 1200, 5)
     out = {}
-    for plan in ("months", "split", "balanced", "dynamic", "months300"):
+    for plan in ("months", "split", "balanced"):
         panel.chunk_split = plan == "split"
-        panel.chunk_policy = {"months": ("months", 1200), "split": None, "balanced": ("balanced", 937),
-                              "dynamic": ("dynamic", 300), "months300": ("months", 300)}[plan]
+        panel.chunk_policy = {"months": ("months", 1200), "split": None, "balanced": ("balanced", 937)}[plan]
         panel.__dict__.pop("_chunk_cache", None)
-        for _ in range(2 if plan == "dynamic" else 1):   # the queue resets itself between launches
-            res = LW.local_stage(panel, LW.PipelineConfig(), LW.table2_models())[0]
+        res = LW.local_stage(panel, LW.PipelineConfig(), LW.table2_models())[0]
         out[plan] = (res.rec.cpu().numpy(), res.status.cpu().numpy())
         if plan == "balanced":
             pl = E._chunk_plan(panel)
             assert pl.nwg == -(-600 * 1200 // 937) and pl.nchunks > pl.nwg
-        if plan == "dynamic":
-            pl = E._chunk_plan(panel)
-            assert pl.nchunks == 2400 and pl.nwg < pl.nchunks and int(pl.queue.abs().sum()) == 0
-    # the dynamic plan's chunks are the months plan's: the same sums, whoever takes them
-    assert _same(out["dynamic"][0], out["months300"][0]) and np.array_equal(out["dynamic"][1], out["months300"][1])
     ra, sa = out["months"]
-    for plan in ("split", "balanced", "dynamic"):
+    for plan in ("split", "balanced"):
         rb, sb = out[plan]
         assert np.array_equal(sa, sb)
         assert _same(ra[..., -1], rb[..., -1])   # N

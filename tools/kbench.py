@@ -23,8 +23,7 @@ def child():
     pol = os.environ.get("KB_POLICY", "")
     if pol == "months":   # whole-month Gram chunks instead of the default plan
         panel.chunk_policy = ("months", panel.max_seg_len)
-    elif pol.startswith("dynamic"):   # dynamic:<rows> -- chunks of <rows> from the queue
-        panel.chunk_policy = ("dynamic", int(pol.split(":")[1]))
+
     if os.environ.get("KB_PLANES") == "1":   # the split panel (fm_split_planes)
         E.split_planes(panel)
     cfg = LW.PipelineConfig()
