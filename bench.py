@@ -205,16 +205,25 @@ def kernel_roofline(step, panel, E, steps):
     reps = 20 if panel.nrows <= 10_000_000 else 3
     dev_ms = {t: E.time_launch(t, reps) for t in tags if t in E.LAST_LAUNCH}
     rows, C = panel.nrows, panel.ncols
-    # algorithmic HBM bytes per launch: every panel column once (8 B per value)
-    # and, for the Gram, the universe level byte
-    cand = {"fm_select_cuts": rows * C * 8, "fm_gram": rows * (C * 8 + 1)}
+    # algorithmic HBM bytes per launch: the Gram reads every panel column once
+    # (8 B per value, from the two 32-bit planes or the FP64 columns) and the universe level
+    # byte.  The roofline is priced on the Gram: it is one kernel, while the select tag is two
+    # launches (the two-wave select, then the fix-up that also computes the universe); the
+    # select's own figure (high plane: 4 B per value; + me, NYSE and level bytes when the
+    # universe comes with it) is reported beside it
+    gram_bytes = rows * (C * 8 + 1)
+    sel_bytes = rows * C * (4 if panel.planes is not None else 8)
     if E.LAST_LAUNCH.get("fm_select_cuts", ("",))[0] == "fm_select_universe":
-        # long months: the universe rides the launch (+ me, the NYSE byte, the level byte)
-        cand["fm_select_cuts"] += rows * (8 + 1 + 1)
-    dom = max((t for t in cand if t in dev_ms), key=lambda k: dev_ms[k])
+        sel_bytes += rows * (8 + 1 + 1)
+    dom = "fm_gram"
     dom_ms = dev_ms[dom]
-    achieved = cand[dom] / (dom_ms * 1e-3) / 1e9
-    return dom, dom_ms, cand[dom], achieved, dev_ms, kern
+    achieved = gram_bytes / (dom_ms * 1e-3) / 1e9
+    sel = None
+    if "fm_select_cuts" in dev_ms:
+        sel = {"launches": "select + fix-up/universe", "bytes_per_launch": sel_bytes, "ms": dev_ms["fm_select_cuts"],
+               "achieved": sel_bytes / (dev_ms["fm_select_cuts"] * 1e-3) / 1e9}
+        sel["frac"] = sel["achieved"] / HBM_PEAK_GBS
+    return dom, dom_ms, gram_bytes, achieved, dev_ms, kern, sel
 
 
 def main():
@@ -262,7 +271,7 @@ def main():
     gres, summ, psumm = out
     nfit = int(((gres.status & 1) != 0).sum().item())   # fitted (month, problem) pairs, all ranks
     ksteps = max(3, min(args.steps, 10)) if workload == "headline" else 2
-    dom, dom_ms, dom_bytes, achieved, dev_ms, kern = kernel_roofline(step, panel, E, ksteps)
+    dom, dom_ms, dom_bytes, achieved, dev_ms, kern, sel_roof = kernel_roofline(step, panel, E, ksteps)
     traffic = _pmc_traffic(dom) if workload == "headline" else None
     ms_step = dt / args.steps * 1e3
     whole = rows_local * B_ROW / (ms_step * 1e-3) / 1e9   # per rank (each rank reads its shard)
@@ -298,7 +307,8 @@ def main():
                      "bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms,
                      "measured_copy_peak": stream, "frac_of_measured_copy": achieved / stream,
                      "whole_pass": {"bytes_per_row": B_ROW, "achieved": whole, "frac": whole / HBM_PEAK_GBS,
-                                    "ms_per_step": ms_step, "per": "rank"}},
+                                    "ms_per_step": ms_step, "per": "rank"},
+                     "select": sel_roof},
         "kernel_ms": {k: round(v, 4) for k, v in dev_ms.items()},
         "lib_sha16": _lib_sha(),
         "kernel_ms_eager_events": {k: round(v, 4) for k, v in kern.items()},

@@ -863,6 +863,31 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
     }
     if (r0 >= cnt) return;                               // block-uniform
     const int r1 = r0 + RROWS < cnt ? r0 + RROWS : cnt;
+    // Predictive slopes, K < 16 (block-uniform): the month moments of ALL of a 16-lane group's
+    // rows (n, Syy and this lane's S column, clamped to a valid row) are loaded here, before
+    // the window rows are staged, so the round trip overlaps the staging and the rolling
+    // sums (the registers cost no occupancy: the workgroup's LDS holds it to 2 per CU).  A
+    // shard with no months of its own has no moments rows at all: nothing to preload.
+    const int K = predictive ? a.prob_k[p] : 0, K1 = K + 1;
+    const int g = tid >> 4, b = tid & 15;
+    constexpr int NIT = RROWS / (FT / 16);   // rows per 16-lane group
+    double scq[NIT][15], n0q[NIT], syq[NIT];
+    if (predictive && K < 16 && a.seg_hi > a.seg_lo) {
+        const int bc = b <= K ? b : 0;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int i = r0 + g + it * (FT / 16);
+            const int s = i < r1 ? ixs[i] : -1;
+            const bool have = i < r1 && s >= a.seg_lo && s < a.seg_hi && i >= a.lag;
+            const int sr = have ? s - a.seg_lo : 0;
+            const double* mo = a.moments + ((int64_t)sr * a.nprob + p) * a.mom_stride;
+            const double* S = mo + 1 + K1;
+#pragma unroll
+            for (int r = 0; r < 15; ++r) scq[it][r] = S[(r < K ? r : 0) * K1 + bc];
+            n0q[it] = mo[0];
+            syq[it] = S[K * K1 + K];
+        }
+    }
     const int q0 = predictive ? (r0 - a.lag > 0 ? r0 - a.lag : 0) : r0;   // rows rolled here
     const int j0 = q0 - a.window + 1 > 0 ? q0 - a.window + 1 : 0;          // rows read
     const int nsrc = r1 - j0, nq = r1 - q0;
@@ -967,31 +992,6 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
     __syncthreads();
     FM_PROBE_AT(ts, 4);
     // predictive slopes: a 16-lane group per row, lane b owns column b of each S row
-    const int K = a.prob_k[p], K1 = K + 1;
-    const int g = tid >> 4, b = tid & 15;
-    constexpr int NIT = RROWS / (FT / 16);   // rows per 16-lane group
-    // K < 16 (block-uniform): the month moments of ALL the group's rows are loaded up front
-    // (n, Syy and this lane's S column, clamped to a valid row), one round trip instead of one
-    // per row
-    double scq[NIT][15], n0q[NIT], syq[NIT];
-    // (a shard with no months of its own has no moments rows at all: nothing to preload, and
-    // no row below is `mine`)
-    if (K < 16 && a.seg_hi > a.seg_lo) {
-        const int bc = b <= K ? b : 0;
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int i = r0 + g + it * (FT / 16);
-            const int s = i < r1 ? ixs[i] : -1;
-            const bool have = i < r1 && s >= a.seg_lo && s < a.seg_hi && i >= a.lag;
-            const int sr = have ? s - a.seg_lo : 0;
-            const double* mo = a.moments + ((int64_t)sr * a.nprob + p) * a.mom_stride;
-            const double* S = mo + 1 + K1;
-#pragma unroll
-            for (int r = 0; r < 15; ++r) scq[it][r] = S[(r < K ? r : 0) * K1 + bc];
-            n0q[it] = mo[0];
-            syq[it] = S[K * K1 + K];
-        }
-    }
     FM_PROBE_AT(ts, 5);
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {     // uniform trip count (shuffles)
