@@ -26,7 +26,7 @@ def main(steps=3):
     del buf
     T, N = (1000, 20000) if os.environ.get("FM_PMC_LONG") == "1" else (600, 5000)   # C5-shaped months
     panel = E.panel_synthetic(T, N, 1, device=dev)
-    if os.environ.get("FM_PLANES") == "1":   # the bench's split panel (fm_split_planes)
+    if os.environ.get("FM_PLANES", "1") == "1":   # the bench's split panel (fm_split_planes; FM_PLANES=0: FP64 columns)
         E.split_planes(panel)
     panel.chunk_policy = E.chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len)   # as bench.make_step
     cfg = LW.PipelineConfig()

@@ -13,7 +13,8 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"select_pair_kernel": "fm_select_cuts", "gram_kernel": "fm_gram",
+KERNELS = {"select_pair_kernel": "fm_select_cuts", "select_pair_hk_kernel": "fm_select_cuts",
+           "select_fixup_universe_kernel": "fm_select_fixup_universe", "gram_kernel": "fm_gram",
            "solve16_kernel": "fm_solve", "probe_kernel": "fm_stream_probe",
            "universe_kernel": "fm_universe", "ts_fused_kernel": "fm_ts_fused"}
 
