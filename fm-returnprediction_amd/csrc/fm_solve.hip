@@ -586,11 +586,15 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
             const double lkk = sqrt(piv);
             const double rinv = 1.0 / lkk;
             const double lik = row[k] * rinv;
+            // unguarded: the entries a guard would keep are never read again -- columns past
+            // the problem's K (and, once k >= K, everything this step touches) are not used by
+            // the back substitution, and a problem whose pivot failed is refactored from G by
+            // the Jacobi path below -- so the two selects per entry are not needed
             static_for<k + 1, G16>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 if (j > kw) return;   // wave-uniform
                 const double sj = rowbc<k + 1>(row[j]) * rinv;   // L[j][k] = S(k)[k][j] / lkk
-                row[j] = go && j <= K ? row[j] - lik * sj : row[j];
+                row[j] = row[j] - lik * sj;
             });
             row[k] = go ? (i == k + 1 ? lkk : lik) : row[k];
             dinv = i == k + 1 ? rinv : dinv;
