@@ -699,7 +699,8 @@ __device__ __forceinline__ int ts_compact_lds(const fm_ts_args& a, int p, int* i
     return base;
 }
 
-__device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs, int cnt, double* xs,
+template <int ML>   // the lags accumulated in the one sweep (the run's NW lags, or MAXL)
+__device__ __forceinline__ void ts_summary_wg_t(const fm_ts_args& a, int p, int k, const int* ixs, int cnt, double* xs,
                               int* wtot, double* dred) {
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
     const double* rk = a.rec + (int64_t)p * a.r_prob + k;
@@ -743,26 +744,26 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
     for (int i = tid; i < n; i += FT) sum += xs[i];
     sum = block_sum<FNW>(sum, dred);
     const double mu = n > 0 ? sum / (double)n : NAN;
-    // gamma_0 .. gamma_min(lags, MAXL) in one sweep, one reduction
-    const int lags = a.nw_lags < MAXL ? a.nw_lags : MAXL;
-    double gl[MAXL + 1];
+    // gamma_0 .. gamma_min(lags, ML) in one sweep, one reduction
+    const int lags = a.nw_lags < ML ? a.nw_lags : ML;
+    double gl[ML + 1];
 #pragma unroll
-    for (int L = 0; L <= MAXL; ++L) gl[L] = 0.0;
+    for (int L = 0; L <= ML; ++L) gl[L] = 0.0;
     for (int i = tid; i < n; i += FT) {
         const double ui = xs[i] - mu;
 #pragma unroll
-        for (int L = 0; L <= MAXL; ++L)
+        for (int L = 0; L <= ML; ++L)
             if (L <= lags && i >= L) gl[L] += ui * (xs[i - L] - mu);
     }
     __syncthreads();   // block_sum's readers are done with dred
 #pragma unroll
-    for (int L = 0; L <= MAXL; ++L) {
+    for (int L = 0; L <= ML; ++L) {
         const double v = wave_sum(gl[L]);
         if (lane == 0) dred[L * FNW + w] = v;
     }
     __syncthreads();
 #pragma unroll
-    for (int L = 0; L <= MAXL; ++L) {
+    for (int L = 0; L <= ML; ++L) {
         double t = 0.0;
 #pragma unroll
         for (int q = 0; q < FNW; ++q) t += dred[L * FNW + q];
@@ -774,9 +775,9 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
         const double wgt = 1.0 - ((double)L / (double)n);
         if (wgt < 0.0) break;
         double gk = 0.0;
-        if (L <= MAXL) {
+        if (L <= ML) {
 #pragma unroll
-            for (int q = 1; q <= MAXL; ++q)
+            for (int q = 1; q <= ML; ++q)
                 if (q == L) gk = gl[q];
         } else {
             for (int i = L + tid; i < n; i += FT) gk += (xs[i] - mu) * (xs[i - L] - mu);
@@ -794,6 +795,14 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
         a.tstat[o] = mu / se;
         a.nobs[o] = n;
     }
+}
+
+// the summary, specialised for the reference's 4 Newey-West lags (the sweep and the reduction
+// carry gamma_0..4 instead of 0..8; identical bits: the extra terms were never accumulated)
+__device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs, int cnt, double* xs,
+                              int* wtot, double* dred) {
+    if (a.nw_lags == 4) ts_summary_wg_t<4>(a, p, k, ixs, cnt, xs, wtot, dred);
+    else ts_summary_wg_t<MAXL>(a, p, k, ixs, cnt, xs, wtot, dred);
 }
 
 // The predictive records' FM summary inside the launch (a.psum_*): workgroup k of the PSK
@@ -1005,7 +1014,9 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
             if (mine && i >= a.lag) {
                 const double* c = rl + (i - a.lag - q0) * PM;
                 bool bad = false;
-                for (int q = 0; q <= K; ++q) bad |= isnan(c[q]);
+#pragma unroll
+                for (int q = 0; q < 16; ++q)   // a fixed trip count: the LDS reads issue together
+                    if (q <= K) bad |= isnan(c[q]);
                 n = n0q[it];
                 ok = !bad && n >= 2.0;
                 if (ok) {
