@@ -542,7 +542,7 @@ __device__ __forceinline__ void hist_select_t(ForEach&& for_each, int nr, const 
                 const uint64_t k = dkey(x);
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (k >= ulo[u] && k <= uhi[u]) {
+                    if (u < nl && k >= ulo[u] && k <= uhi[u]) {   // nl: block-uniform (usually 2)
                         const uint32_t pos = atomicAdd(&sm.hcnt[u], 1u);
                         if (pos < (uint32_t)CAP) sm.buf[u * CAP + pos] = k;
                     }
