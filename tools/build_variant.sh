@@ -10,11 +10,15 @@ CS=$ROOT/fm-returnprediction_amd/csrc
 VD=$ROOT/build_variants/$name
 mkdir -p "$VD/obj"
 cp -p "$CS"/build/*.o "$VD/obj/"
+pids=()
 for src in "$@"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I"$ROOT/include" \
     -Wall -Wno-unused-function $flags -c "$CS/$src" -o "$VD/obj/${src%.hip}.o" &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do
+  wait "$p" || { echo "build_variant: a compile failed" >&2; rm -rf "$VD"; exit 1; }
+done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$VD"/obj/*.o -o "$VD/libfm_hip.so"
 rm -rf "$VD/obj"
 echo "$VD/libfm_hip.so"
