@@ -657,7 +657,15 @@ namespace {
 
 constexpr int FT = 256;
 constexpr int FNW = FT / WAVE;
-constexpr int RROWS = 64;    // rows per rolling workgroup (4 predictive rows per wave pass)
+// rows per rolling workgroup (RROWS / 16 predictive rows per 16-lane group): the shortest
+// chain per workgroup wins -- 16 rows 11.8 us, 32 rows 15.8 us, 64 rows 19.4 us for the bench's
+// 600 x 11 series (profiles/r05/v9_kbench_ts_rrows.log): more workgroups each stage more window
+// rows, but a workgroup's serial work (prefix sums, rolling means, predictive rows) shrinks
+#ifndef FM_TS_RROWS
+#define FM_TS_RROWS 16
+#endif
+constexpr int RROWS = FM_TS_RROWS;
+static_assert(RROWS % 16 == 0, "fm_ts_fused: RROWS is a multiple of the 16 row groups");
 constexpr int MAXL = 8;      // Newey-West lags accumulated in one sweep
 
 __host__ __device__ __forceinline__ size_t ts_ix_bytes(int T) { return ((size_t)T * 4 + 15) & ~(size_t)15; }
