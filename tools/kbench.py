@@ -23,6 +23,8 @@ def child():
     pol = os.environ.get("KB_POLICY", "")
     if pol == "months":   # whole-month Gram chunks instead of the default plan
         panel.chunk_policy = ("months", panel.max_seg_len)
+    if os.environ.get("KB_SLOTS"):   # the balanced plan cut for this many workgroups
+        panel.chunk_policy = E.chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len, slots=int(os.environ["KB_SLOTS"]))
 
     if os.environ.get("KB_PLANES") == "1":   # the split panel (fm_split_planes)
         E.split_planes(panel)
@@ -52,7 +54,7 @@ def main():
             continue
         d = json.loads(line[0][3:])
         tag = os.path.basename(os.path.dirname(lib)) + (f"[chunk {os.environ['KB_CHUNK']}]" if os.environ.get("KB_CHUNK") else "")
-        tag += "".join(f"[{k}={os.environ[k]}]" for k in ("KB_POLICY", "KB_PLANES", "KB_PSUM") if os.environ.get(k))
+        tag += "".join(f"[{k}={os.environ[k]}]" for k in ("KB_POLICY", "KB_PLANES", "KB_PSUM", "KB_SLOTS") if os.environ.get(k))
         print(tag, " ".join(f"{k}={v * 1e3:.1f}us" for k, v in d.items()), flush=True)
 
 
