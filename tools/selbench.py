@@ -18,6 +18,8 @@ def child():
     E.require_device()
     T, N = int(os.environ.get("SB_T", "1000")), int(os.environ.get("SB_N", "20000"))
     p = E.panel_synthetic(T, N, 20150101, month0=50000)
+    if os.environ.get("SB_PLANES", "1") == "1":   # the bench's split panel (high-plane selects)
+        E.split_planes(p)
     for _ in range(2):
         E.select_cuts(p, 0.01, 0.99, 5, center=True)
     torch.cuda.synchronize()
