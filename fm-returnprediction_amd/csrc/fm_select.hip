@@ -1470,6 +1470,10 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
 #ifndef FM_PAIR_HK_PF
 #define FM_PAIR_HK_PF 1
 #endif
+// 1: the valid-key count as a per-lane carry count and one wave sum (0: a ballot per value)
+#ifndef FM_PAIR_HK_LANECNT
+#define FM_PAIR_HK_LANECNT 1
+#endif
 constexpr int pair_hk_wgs(int vph) {
     return FM_PAIR_HK_WGS > 0 ? FM_PAIR_HK_WGS : (vph <= 16 ? 12 : (vph <= 24 ? 10 : 8));
 }
@@ -1620,6 +1624,25 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
         const int lim = L - row0;
         int nh = 0;
         uint32_t kmn = HK_NONE, kmx2 = 0;
+#if FM_PAIR_HK_LANECNT
+        // invalid keys counted per lane from the wrap of the max's offset add (one add with
+        // carry per value), one wave sum after the loop instead of a ballot per value
+        int nbad = 0;
+#pragma unroll
+        for (int v = 0; v < VPH; ++v) {
+            const uint32_t kk = v * 2 * WAVE < lim ? hkey(xk[v]) : HK_NONE;
+            xk[v] = kk;
+            kmn = min(kmn, kk);
+            uint32_t kx;   // kk + 0x1FFFFE: NaN / absent keys wrap below every valid one (carry set)
+            asm volatile("v_add_co_u32 %0, vcc, 0x1ffffe, %2\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+                         : "=&v"(kx), "+v"(nbad)
+                         : "v"(kk)
+                         : "vcc");
+            kmx2 = max(kmx2, kx);
+            asm volatile("" : "+v"(kmn), "+v"(kmx2));
+        }
+        nh = VPH * WAVE - wave_sum(nbad);
+#else
 #pragma unroll
         for (int v = 0; v < VPH; ++v) {
             const uint32_t kk = v * 2 * WAVE < lim ? hkey(xk[v]) : HK_NONE;
@@ -1629,6 +1652,7 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
             kmx2 = max(kmx2, kk + 0x1FFFFEu);   // NaN / absent keys wrap below every valid one
             asm volatile("" : "+s"(nh), "+v"(kmn), "+v"(kmx2));
         }
+#endif
         const bool tvalid = kmn <= HK_MAX;
         const uint32_t kmx = kmx2 - 0x1FFFFEu;
         const bool amb = tvalid && (kmn == 0u || kmx == HK_MAX);
