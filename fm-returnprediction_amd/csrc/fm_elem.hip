@@ -150,12 +150,28 @@ __global__ __launch_bounds__(ET) void gen_kernel(uint64_t seed, int64_t month0, 
     nyse[cell] = cell_hash(seed, m, f, 66) < nyse_thr ? 1 : 0;
 }
 
+// The achievable HBM READ rate (bench.py's measured_copy_peak for the read-dominated Gram):
+// 16-byte loads, PU of them in flight per thread, grid-stride over the buffer; the sum keeps
+// the loads.  n must be a multiple of 2 (double2 pairs) for the full rate; an odd tail is
+// read by thread 0.
+constexpr int PU = 4;
 __global__ __launch_bounds__(ET) void probe_kernel(const double* __restrict__ src, int64_t n,
                                                    double* __restrict__ out) {
     __shared__ double red[ET / WAVE];
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+    const int64_t np = n / 2;
+    const int64_t stride = (int64_t)gridDim.x * ET;
     double s = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * ET + threadIdx.x; i < n; i += (int64_t)gridDim.x * ET)
-        s += src[i];
+    int64_t i = (int64_t)blockIdx.x * ET + threadIdx.x;
+    for (; i + (PU - 1) * stride < np; i += PU * stride) {
+        double2 v[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) v[u] = s2[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) s += v[u].x + v[u].y;
+    }
+    for (; i < np; i += stride) s += s2[i].x + s2[i].y;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) s += src[n - 1];
     s = block_sum<ET / WAVE>(s, red);
     if (threadIdx.x == 0) atomicAdd(out, s);
 }
@@ -290,7 +306,8 @@ extern "C" int fm_split_planes(const double* cols, int64_t col_stride, int32_t n
 extern "C" int fm_stream_probe(const double* src, int64_t n, double* out, void* stream) {
     using namespace fm;
     FM_REQUIRE(src && out, "fm_stream_probe: null pointer");
-    hipLaunchKernelGGL(probe_kernel, dim3(2048), dim3(ET), 0, (hipStream_t)stream, src, n, out);
+    FM_REQUIRE(((uintptr_t)src & 15) == 0, "fm_stream_probe: src must be 16-byte aligned");
+    hipLaunchKernelGGL(probe_kernel, dim3(256 * 8), dim3(ET), 0, (hipStream_t)stream, src, n, out);
     FM_CHECK_LAUNCH("fm_stream_probe");
     return FM_OK;
 }

@@ -228,14 +228,20 @@ __device__ __forceinline__ void fixup_body(const SelArgs& a, double* zs, int zs_
     SelArgs b = a;
     b.ctl = nullptr;
     FM_PROBE_AT(sel, 4);
-    const uint32_t nw = __hip_atomic_load(&ctl->nwork, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t nw0 = __hip_atomic_load(&ctl->nwork, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // an empty list (every workgroup reads the same count: nothing appends during this launch)
     // needs no reset: exit without touching the done counter (256 same-address atomics cost
     // more than the whole no-op launch)
     FM_PROBE_AT(sel, 5);
-    if (nw == 0) return;
+    if (nw0 == 0) return;
+    // a list left over by a call whose fix-up never ran (an error between the launches) may
+    // hold more entries than this call's units, or ids of a larger shape: both are bounded
+    // here (a stale in-range id only redoes that unit exactly: same result)
+    const uint32_t nunits = (uint32_t)((int64_t)b.nseg * b.ncols);
+    const uint32_t nw = nw0 < nunits ? nw0 : nunits;
     for (uint32_t i = bid; i < nw; i += nblk) {
         const uint32_t u = ctl->work[i];
+        if (u >= nunits) continue;   // workgroup-uniform
         const int s = (int)(u % (uint32_t)b.nseg), c = (int)(u / (uint32_t)b.nseg);
         if constexpr (VPT > 0) select_unit_wg<VPT>(b, s, c, sm.sel);
         else stream_unit(b, s, c, sm.sel);

@@ -88,11 +88,14 @@ struct SelArgs {
 };
 
 // One lane: unit u goes on the fix-up kernel's worklist (and is marked, nvalid = -1, when the
-// kernel could not finish it).
+// kernel could not finish it).  A call pushes each of its nseg * ncols units at most once, so
+// the list (sized for them) cannot overflow -- unless an earlier call's entries were left
+// behind (its fix-up launch never ran: an error between the two launches).  Entries past the
+// list's capacity are then dropped here, and the fix-up skips ids outside this call's units.
 __device__ __forceinline__ void sel_push(const SelArgs& a, int64_t u) {
     if (a.ctl != nullptr) {
         const uint32_t i = atomicAdd(&a.ctl->nwork, 1u);
-        a.ctl->work[i] = (uint32_t)u;
+        if (i < (uint32_t)((int64_t)a.nseg * a.ncols)) a.ctl->work[i] = (uint32_t)u;
     }
 }
 __device__ __forceinline__ void sel_mark(const SelArgs& a, int64_t u) {

@@ -373,6 +373,11 @@ __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t 
 // Sixteen lanes per (problem, fitted-month row), sixteen rows per workgroup: lane a owns
 // regressor a (K <= 15), the quadratic forms c'Sxx c and c'Sxy are 16-lane sums.  Most rows
 // of a gathered series belong to other ranks' months and only write the zero record.
+//
+// The zero record of another rank's month is -0.0, not +0.0: the SUM all-reduce that merges
+// the ranks' records (fmcore.dist.combine_predictive) then returns the owner's value bit for
+// bit, a signed zero included (v + (-0.0) == v for every v, -0.0 itself too; with +0.0
+// fillers an owner's -0.0 would come back +0.0), in any summation order.
 constexpr int PG = 16;
 __global__ __launch_bounds__(TT) void predictive_kernel(const double* mom, int mom_stride,
                                                         int nseg, int nprob,
@@ -425,8 +430,8 @@ __global__ __launch_bounds__(TT) void predictive_kernel(const double* mom, int m
         if (!(tb > 0.0)) st |= FM_ST_CONST_COL;
     }
     if (row && lane == 0) {
-        if (other) {   // zero record for the sum-combine of sharded runs
-            o[0] = o[1] = o[2] = o[3] = 0.0;
+        if (other) {   // -0.0 record for the sum-combine of sharded runs (exact, signs kept)
+            o[0] = o[1] = o[2] = o[3] = -0.0;
             pst[(int64_t)p * nseg + ic] = 0;
         } else {
             o[0] = slope;
@@ -489,8 +494,8 @@ __global__ __launch_bounds__(WAVE) void predictive_kernel_wide(const double* mom
     const int cnt = count[p];
     const int s = i < cnt ? idx[(int64_t)p * nseg + i] : -1;
     if (i < cnt && (s < seg_lo || s >= seg_hi)) {
-        // another rank's month (sharded runs): zero record for the sum-combine
-        if (lane < 4) o[lane] = 0.0;
+        // another rank's month (sharded runs): -0.0 record for the exact sum-combine
+        if (lane < 4) o[lane] = -0.0;
         if (lane == 0) pst[(int64_t)p * nseg + i] = 0;
         return;
     }
@@ -813,52 +818,6 @@ __device__ void ts_summary_wg(const fm_ts_args& a, int p, int k, const int* ixs,
     else ts_summary_wg_t<MAXL>(a, p, k, ixs, cnt, xs, wtot, dred);
 }
 
-// The predictive records' FM summary inside the launch (a.psum_*): workgroup k of the PSK
-// extra workgroups of problem p summarizes field k of p's predictive records with the same
-// code as the separate launch on them (ts_compact_lds + ts_summary_wg: the same bits), once
-// every rolling workgroup of p has counted itself done in a.psum_ctr[p].  It waits only on
-// workgroups of lower linear id (dispatched before it), and fm_ts_fused folds the summary in
-// only when the whole grid is co-resident, so the wait always ends; the counter is reset by
-// the last of the PSK summary workgroups for the next launch.
-constexpr int PSK = 3;   // summarized fields of a predictive record (slope, R^2, n)
-
-__device__ void ts_pred_summary_wg(const fm_ts_args& a, int p, int k, int nroll, int* ixs, double* lds_d,
-                                   int* wtot, double* dred) {
-    if (threadIdx.x == 0) {
-        uint32_t spins = 0;   // bounded: a grid that drains is worth more than a hung one
-        while (__hip_atomic_load(&a.psum_ctr[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)nroll &&
-               ++spins < (1u << 24))
-            __builtin_amdgcn_s_sleep(2);
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the rolling workgroups' records
-    fm_ts_args b = a;
-    b.rec = a.pred;
-    b.r_seg = 4;
-    b.r_prob = (int64_t)a.nseg * 4;
-    b.status = a.pred_status;
-    b.s_seg = 1;
-    b.s_prob = a.nseg;
-    b.kmax = PSK;
-    b.idx = a.psum_idx;
-    b.count = a.psum_count;
-    b.mean = a.psum_mean;
-    b.se = a.psum_se;
-    b.tstat = a.psum_tstat;
-    b.nobs = a.psum_nobs;
-    const int cnt = ts_compact_lds(b, p, ixs, wtot);
-    if (k == 0) {
-        for (int i = threadIdx.x; i < cnt; i += FT) b.idx[(int64_t)p * b.nseg + i] = ixs[i];
-        if (threadIdx.x == 0) b.count[p] = cnt;
-    }
-    ts_summary_wg(b, p, k, ixs, cnt, lds_d, wtot, dred);
-    if (threadIdx.x == 0) {   // every thread of this workgroup is past its read of the counter
-        const uint32_t t = atomicAdd(&a.psum_ctr[p], 1u);
-        if (t == (uint32_t)(nroll + PSK - 1))
-            __hip_atomic_store(&a.psum_ctr[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* ixs, int cnt,
                               double* lds_d) {
     const int tid = threadIdx.x;
@@ -1068,8 +1027,8 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
             uint32_t st = 0;
             double slope = NAN, r2 = NAN, nn = NAN;
             if (!mine) {
-                // another rank's month (sharded runs): zero record for the sum-combine
-                slope = r2 = nn = 0.0;
+                // another rank's month (sharded runs): -0.0 record for the exact sum-combine
+                slope = r2 = nn = -0.0;
             } else if (ok) {
                 slope = ty / tb;
                 r2 = (ty * ty) / (tb * syy);
@@ -1080,7 +1039,7 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
             o[0] = slope;
             o[1] = r2;
             o[2] = nn;
-            o[3] = 0.0;
+            o[3] = mine ? 0.0 : -0.0;
             a.pred_status[(int64_t)p * T + i] = st;
         }
     }
@@ -1094,12 +1053,6 @@ __global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {
     int* ixs = reinterpret_cast<int*>(lds);
     double* lds_d = lds + ts_ix_bytes(a.nseg) / 8;
     FM_PROBE_AT(ts, 0);
-    const int nroll = a.roll ? (a.nseg + RROWS - 1) / RROWS : 0;
-    if (a.psum_mean != nullptr && bx >= a.kmax + nroll) {   // block-uniform
-        ts_pred_summary_wg(a, p, bx - a.kmax - nroll, nroll, ixs, lds_d, wtot, dred);
-        FM_PROBE_AT(ts, 7);
-        return;
-    }
     const int cnt = ts_compact_lds(a, p, ixs, wtot);
     FM_PROBE_AT(ts, 1);
     if (bx == 0) {
@@ -1111,13 +1064,6 @@ __global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {
     } else {
         ts_rolling_wg(a, p, bx - a.kmax, ixs, cnt, lds_d);
         FM_PROBE_AT(ts, 6);
-        if (a.psum_mean != nullptr) {   // this problem's predictive summary waits for the count
-            __syncthreads();           // every pred / pred_status write of the workgroup issued
-            if (threadIdx.x == 0) {
-                __threadfence();
-                atomicAdd(&a.psum_ctr[p], 1u);
-            }
-        }
     }
     FM_PROBE_AT(ts, 7);
 }
@@ -1151,9 +1097,6 @@ extern "C" int fm_ts_fused(const fm_ts_args* args, void* stream) {
     FM_REQUIRE(a.pred == nullptr || (a.roll && a.moments && a.prob_k && a.pred_status && a.lag >= 1),
                "fm_ts_fused: the predictive stage needs roll, moments, prob_k, pst and lag >= 1");
     if (a.nprob == 0 || a.nseg == 0) return FM_OK;
-    FM_REQUIRE(a.psum_mean == nullptr || (a.pred && a.psum_idx && a.psum_count && a.psum_se && a.psum_tstat &&
-                                           a.psum_nobs && a.psum_ctr),
-               "fm_ts_fused: the predictive summary needs pred and every psum_* buffer");
     const size_t lds = fm_ts_fused_lds_bytes(a.nseg, a.pmax, a.window, a.lag, a.roll != nullptr,
                                              a.pred != nullptr);
     FM_REQUIRE(lds <= FM_TS_FUSED_MAX_LDS,
@@ -1169,52 +1112,7 @@ extern "C" int fm_ts_fused(const fm_ts_args* args, void* stream) {
         }
     }
     const int nchunk = a.roll ? (a.nseg + RROWS - 1) / RROWS : 0;
-    if (a.psum_mean == nullptr) {
-        hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk, a.nprob), dim3(FT), lds, (hipStream_t)stream, a);
-        FM_CHECK_LAUNCH("fm_ts_fused");
-        return FM_OK;
-    }
-    // the predictive summary's workgroups wait on the rolling ones: only when every workgroup
-    // of the grid is resident at once; otherwise a second launch on the records, same result
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        FM_REQUIRE(hipGetDevice(&dev) == hipSuccess &&
-                       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
-                   "fm_ts_fused: cannot query the device");
-    }
-    int per_cu = 0;
-    FM_REQUIRE(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ts_fused_kernel, FT, lds) ==
-                   hipSuccess, "fm_ts_fused: occupancy query failed");
-    const int64_t grid = (int64_t)(a.kmax + nchunk + PSK) * a.nprob;
-    if (grid <= (int64_t)per_cu * cus) {
-        hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk + PSK, a.nprob), dim3(FT), lds,
-                           (hipStream_t)stream, a);
-        FM_CHECK_LAUNCH("fm_ts_fused");
-        return FM_OK;
-    }
-    fm_ts_args m = a;
-    m.psum_idx = m.psum_count = m.psum_nobs = nullptr;
-    m.psum_mean = m.psum_se = m.psum_tstat = nullptr;
-    m.psum_ctr = nullptr;
-    hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk, a.nprob), dim3(FT), lds, (hipStream_t)stream, m);
+    hipLaunchKernelGGL(ts_fused_kernel, dim3(a.kmax + nchunk, a.nprob), dim3(FT), lds, (hipStream_t)stream, a);
     FM_CHECK_LAUNCH("fm_ts_fused");
-    fm_ts_args q{};
-    q.rec = a.pred;
-    q.r_seg = 4;
-    q.r_prob = (int64_t)a.nseg * 4;
-    q.status = a.pred_status;
-    q.s_seg = 1;
-    q.s_prob = a.nseg;
-    q.nseg = a.nseg;
-    q.nprob = a.nprob;
-    q.kmax = PSK;
-    q.nw_lags = a.nw_lags;
-    q.idx = a.psum_idx;
-    q.count = a.psum_count;
-    q.mean = a.psum_mean;
-    q.se = a.psum_se;
-    q.tstat = a.psum_tstat;
-    q.nobs = a.psum_nobs;
-    return fm_ts_fused(&q, stream);
+    return FM_OK;
 }

@@ -72,9 +72,6 @@ class TsArgs(C.Structure):
         ("work", _p), ("window", _i32), ("min_periods", _i32), ("pmax", _i32), ("roll", _p),
         ("moments", _p), ("mom_stride", _i32), ("prob_k", _p), ("lag", _i32), ("seg_lo", _i32),
         ("seg_hi", _i32), ("pred", _p), ("pred_status", _p),
-        # the predictive records' summary in the same launch (psum_mean None: not here)
-        ("psum_idx", _p), ("psum_count", _p), ("psum_mean", _p), ("psum_se", _p), ("psum_tstat", _p),
-        ("psum_nobs", _p), ("psum_ctr", _p),
     ]
 
 

@@ -1,4 +1,5 @@
-"""pandas <-> device glue shared by the drop-in modules (src/regressions.py,
+"""pandas <-> device glue shared by the drop-in modules (fmdrop/regressions.py,
+fmdrop/calc_Lewellen_2014.py, mirroring the reference's src/regressions.py and
 src/calc_Lewellen_2014.py): panel marshaling, reference-exact error behaviour and
 result frames.  Compute happens only in libfm_hip kernels (fmcore.engine)."""
 from __future__ import annotations

@@ -468,13 +468,9 @@ def default_chunk_rows(total_rows, nseg, max_seg_len, target_chunks=512):
 
 
 GRAM_SLOTS_PER_CU = 3   # fm_gram workgroups resident per CU (3 waves / SIMD)
-
-
-def _num_cus():
-    try:
-        return torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    except Exception:
-        return 256
+# The plan's slot count is a constant of the plan, not a query of the local device: a plan
+# (and so every month's FP64 partial-sum order) must not change with the GPU a rank runs on.
+GRAM_PLAN_SLOTS = 256 * GRAM_SLOTS_PER_CU   # MI355X: 256 CUs
 
 
 def chunk_policy(total_rows, nseg, max_seg_len, slots=None, min_rows=2048):
@@ -488,8 +484,10 @@ def chunk_policy(total_rows, nseg, max_seg_len, slots=None, min_rows=2048):
       grid of whole months leaves 88 CUs a third month to finish while the rest idle
       (profiles/r04/v1_size_scan.log: 600 months cost what 768 do).
     * ("months", chunk_rows): otherwise months split into ceil(L / chunk_rows) chunks
-      (default_chunk_rows), one per workgroup."""
-    slots = slots or _num_cus() * GRAM_SLOTS_PER_CU
+      (default_chunk_rows), one per workgroup.
+
+    ``slots`` defaults to GRAM_PLAN_SLOTS (a constant, never the local device's CU count)."""
+    slots = slots or GRAM_PLAN_SLOTS
     if nseg > 0 and nseg < 4 * slots:
         R = -(-int(total_rows) // slots)
         if R >= min_rows:
@@ -907,27 +905,12 @@ def ts_fused_fits(nseg, pmax=0, window=None, lag=1, predictive=False):
     return need <= L.FM_TS_FUSED_MAX_LDS
 
 
-_PSUM_CTR = {}
-
-
-def _psum_ctr(dev, nprob):
-    """Arrival counters of fm_ts_fused's in-launch predictive summary: zeroed once, every
-    launch leaves them zero (one buffer per device and problem count, reused by the graphs)."""
-    key = (str(dev), nprob)
-    if key not in _PSUM_CTR:
-        _PSUM_CTR[key] = torch.zeros(max(nprob, 1), dtype=torch.int32, device=dev)
-    return _PSUM_CTR[key]
-
-
 def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_lags=4,
              window=None, min_periods=None, pmax=None, moments=None, mom_stride=0, prob_k=None,
-             lag=1, seg_lo=0, seg_hi=None, predictive=False, pred_summary=False, tag="fm_ts_fused"):
+             lag=1, seg_lo=0, seg_hi=None, predictive=False, tag="fm_ts_fused"):
     """The whole time-series stage in one launch (fm_ts_fused): TSIndex, Summary and, when
     ``window`` is given, the rolling means [P, T, pmax]; with ``predictive`` also the
-    predictive records [P, T, 4] and status [P, T].  Returns (ix, summ, roll, pred, pst);
-    with ``pred_summary`` (predictive, no exchange before the summary) a sixth element, the
-    predictive records' (Summary, TSIndex) -- summarize_predictive's result, bit for bit --
-    from the same launch (three more workgroups per problem wait for its rolling ones)."""
+    predictive records [P, T, 4] and status [P, T].  Returns (ix, summ, roll, pred, pst)."""
     dev = rec.device
     idx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
     cnt = torch.empty(nprob, dtype=torch.int32, device=dev)
@@ -947,38 +930,19 @@ def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_la
                   min_periods=min_periods or 0, pmax=pmax or 0, roll=_ptr(roll), moments=_ptr(moments),
                   mom_stride=mom_stride, prob_k=_ptr(prob_k), lag=lag, seg_lo=seg_lo,
                   seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst))
-    psum, pbufs = None, ()
-    if pred_summary:
-        if not predictive:
-            raise ValueError("pred_summary needs predictive")
-        pidx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
-        pcnt = torch.empty(nprob, dtype=torch.int32, device=dev)
-        pmean = torch.empty((nprob, 3), dtype=torch.float64, device=dev)
-        pse, pts = torch.empty_like(pmean), torch.empty_like(pmean)
-        pnobs = torch.empty((nprob, 3), dtype=torch.int32, device=dev)
-        ctr = _psum_ctr(dev, nprob)
-        ta.psum_idx, ta.psum_count, ta.psum_mean = pidx.data_ptr(), pcnt.data_ptr(), pmean.data_ptr()
-        ta.psum_se, ta.psum_tstat, ta.psum_nobs, ta.psum_ctr = (pse.data_ptr(), pts.data_ptr(), pnobs.data_ptr(),
-                                                                 ctr.data_ptr())
-        psum = (Summary(pmean, pse, pts, pnobs), TSIndex(pidx, pcnt))
-        pbufs = (pidx, pcnt, pmean, pse, pts, pnobs, ctr)
     _kcall(tag, "fm_ts_fused", L.C.byref(ta), _stream())
     _remember(tag, "fm_ts_fused", ta, rec, status, idx, cnt, mean, se, ts, nobs, roll,
-              moments, prob_k, pred, pst, *pbufs)
-    out = (TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst)
-    return out + (psum,) if pred_summary else out
+              moments, prob_k, pred, pst)
+    return TSIndex(idx, cnt), Summary(mean, se, ts, nobs), roll, pred, pst
 
 
 def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag=1, seg_lo=0,
-                       seg_hi=None, moments=None, rolling=True, predictive=True, pred_summary=False):
+                       seg_hi=None, moments=None, rolling=True, predictive=True):
     """compact_result + summarize_result + rolling_result + predictive_result in one launch.
-    Returns (ix, summ, roll, pred, pst); with ``pred_summary`` (predictive runs without an
-    exchange of the predictive records) also the predictive (Summary, TSIndex) as a sixth
-    element, from the same launch where it fits."""
+    Returns (ix, summ, roll, pred, pst)."""
     T, P, rs = res.rec.shape
     mom = res.moments if moments is None else moments
     window = window if (rolling or predictive) else None
-    pred_summary = bool(pred_summary and predictive)
     if not ts_fused_fits(T, res.pmax, window, lag, predictive):
         ix = compact_result(res)
         summ, _ = summarize_result(res, ix, nw_lags)
@@ -987,14 +951,12 @@ def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag
             roll = rolling_result(res, ix, window, min_periods)
         if predictive:
             pred, pst = predictive_result(res, ix, roll, lag, seg_lo, seg_hi, moments)
-        out = (ix, summ, roll, pred, pst)
-        return out + (summarize_predictive(pred, pst, nw_lags),) if pred_summary else out
+        return ix, summ, roll, pred, pst
     pk = _small_tensor(tuple(p.K for p in res.problems), torch.int32, res.rec.device) if predictive else None
     return ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
                     window=window, min_periods=min_periods,
                     pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
-                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive,
-                    pred_summary=pred_summary)
+                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive)
 
 
 def forecast(panel: DevicePanel, coef, cols=None):
@@ -1125,6 +1087,12 @@ def rolling_beta(day, ri, rm, seg_off, q_seg, q_day0, q_day1, period_weeks=156):
 
 
 def stream_probe(t):
+    """fm_stream_probe: the sum of a contiguous, 16-byte aligned float64 tensor read as a
+    plain HBM stream (bench.py's measured read rate; re-issued by time_launch)."""
+    if t.dtype != torch.float64 or not t.is_contiguous() or t.data_ptr() % 16:
+        raise ValueError("stream_probe: a contiguous, 16-byte aligned float64 tensor")
     out = torch.zeros(1, dtype=torch.float64, device=t.device)
-    _kcall("fm_stream_probe", "fm_stream_probe", t.data_ptr(), t.numel(), out.data_ptr(), _stream())
+    args = (t.data_ptr(), t.numel(), out.data_ptr())
+    _kcall("fm_stream_probe", "fm_stream_probe", *args, _stream())
+    LAST_LAUNCH["fm_stream_probe"] = ("fm_stream_probe", None, ((t, out), args))
     return out

@@ -163,35 +163,21 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
     return res, names, cuts, level, bp
 
 
-# The predictive summary inside the time-series launch (fm_ts_args.psum_*, bit-identical):
-# 31.2 us for the one launch against 19.5 + 9.5 us for two on the bench panel
-# (profiles/r05/v3_*), so world-1 runs keep the second launch.
-PRED_SUMMARY_IN_LAUNCH = False
-
-
-def time_series_stage(res: E.FMResult, cfg: PipelineConfig, moments=None, seg_lo=0, seg_hi=None,
-                      pred_summary=False):
+def time_series_stage(res: E.FMResult, cfg: PipelineConfig, moments=None, seg_lo=0, seg_hi=None):
     """One launch (fm_ts_fused): compaction, FM summaries, rolling means, predictive slopes.
-    Their FM summary follows in summarize_predictive -- or, with ``pred_summary`` (no exchange
-    of the predictive records in between), comes from the same launch as a sixth element
-    (psumm, pix).  Returns (ix, summ, roll, pred, pst[, (psumm, pix)])."""
-    out = E.time_series_result(
+    Their FM summary follows in summarize_predictive.  Returns (ix, summ, roll, pred, pst)."""
+    return E.time_series_result(
         res, cfg.nw_lags, cfg.window, cfg.min_periods, cfg.lag, seg_lo=seg_lo, seg_hi=seg_hi,
-        moments=moments, rolling=cfg.forecasts or cfg.fig1, predictive=cfg.forecasts,
-        pred_summary=pred_summary and cfg.forecasts)
-    if pred_summary and len(out) == 5:
-        out = out + (None,)
-    return out
+        moments=moments, rolling=cfg.forecasts or cfg.fig1, predictive=cfg.forecasts)
 
 
 def run_pipeline(panel: E.DevicePanel, cfg: PipelineConfig = None, model_cols=None, y="retx"):
     cfg = cfg or PipelineConfig()
     model_cols = model_cols or table2_models()
     res, names, cuts, level, bp = local_stage(panel, cfg, model_cols, y)
-    out = time_series_stage(res, cfg, pred_summary=PRED_SUMMARY_IN_LAUNCH)
-    ix, summ, roll, pred, pst = out[:5]
-    psumm = out[5][0] if len(out) > 5 and out[5] is not None else None
-    if psumm is None and cfg.forecasts:
+    ix, summ, roll, pred, pst = time_series_stage(res, cfg)
+    psumm = None
+    if cfg.forecasts:
         psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
     return PipelineResult(model_names=names, model_cols=dict(model_cols, **({"Figure 1": FIG1_VARS} if cfg.fig1 else {})),
                           res=res, ix=ix, summary=summ, rolling=roll, pred=pred, pred_status=pst,

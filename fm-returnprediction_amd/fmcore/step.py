@@ -65,12 +65,8 @@ class ShardedStep:
         if self.exchange:
             gres = E.FMResult(problems=res.problems, rec=self.rec_g, status=self.st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
-        # without an exchange of the predictive records the launch can also give their summary
-        # (PRED_SUMMARY_IN_LAUNCH; measured slower than its own launch, so off)
-        out = LW.time_series_stage(gres, self.cfg, moments=res.moments, seg_lo=self.seg_lo,
-                                   seg_hi=self.seg_hi, pred_summary=LW.PRED_SUMMARY_IN_LAUNCH and not self.exchange)
-        ix, summ, roll, pred, pst = out[:5]
-        self._psum = out[5] if len(out) > 5 else None
+        ix, summ, roll, pred, pst = LW.time_series_stage(gres, self.cfg, moments=res.moments,
+                                                         seg_lo=self.seg_lo, seg_hi=self.seg_hi)
         return gres, summ, pred, pst
 
     def exchange_pred(self, pred, pst):
@@ -80,8 +76,6 @@ class ShardedStep:
     def phase_pred(self, pred, pst):
         if pred is None:
             return None
-        if not self.exchange and getattr(self, "_psum", None) is not None:
-            return self._psum[0]   # came with phase_ts's launch
         psumm, _ = E.summarize_predictive(pred, pst, self.cfg.nw_lags)
         return psumm
 

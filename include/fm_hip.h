@@ -3,8 +3,8 @@
  *
  * Drop-in boundary.  The reference (BaileyMeche/FM-ReturnPrediction) has no FFI layer: its
  * hot path is a set of pandas-in/pandas-out Python functions.  The Python mirror in
- * fm-returnprediction_amd/src/{regressions,calc_Lewellen_2014}.py keeps those names and
- * signatures and calls the entry points below through ctypes.  Each entry point names
+ * fm-returnprediction_amd/fmdrop/{regressions,calc_Lewellen_2014,transform_compustat}.py
+ * keeps those names and signatures and calls the entry points below through ctypes.  Each entry point names
  * the reference computation it replaces:
  *
  *   fm_select_cuts  <- np.percentile(vals, 1/99) per month per var
@@ -360,20 +360,6 @@ typedef struct fm_ts_args {
     int32_t lag, seg_lo, seg_hi;
     double* pred;                 /* [nprob][nseg][4] or NULL */
     uint32_t* pred_status;        /* [nprob][nseg] */
-    /* The predictive records' FM summary inside this launch (runs with no exchange between
-     * the two stages): with psum_mean set (pred set too), three more workgroups per problem
-     * wait until the problem's rolling workgroups are done, then compact its pred_status and
-     * summarize the first 3 fields of its pred records -- what fm_ts_fused on (pred, 4,
-     * nseg*4, pred_status, 1, nseg, nseg, nprob, kmax 3) returns, bit for bit.  When the grid
-     * would not be resident at once, a second launch does exactly that.  All NULL
-     * (zero-initialised): no predictive summary here. */
-    int32_t* psum_idx;            /* [nprob][nseg] */
-    int32_t* psum_count;          /* [nprob] */
-    double* psum_mean;            /* [nprob][3] */
-    double* psum_se;
-    double* psum_tstat;
-    int32_t* psum_nobs;
-    uint32_t* psum_ctr;           /* [nprob] arrival counters: zero before the first launch, left zero */
 } fm_ts_args;
 
 /* LDS bytes the fused launch stages per workgroup; it must not exceed FM_TS_FUSED_MAX_LDS

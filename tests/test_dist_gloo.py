@@ -45,14 +45,20 @@ def _worker(rank, world, port, T, P, rs, q):
     counts = [e - s for s, e in bounds]
     g_rec, g_st = D.gather_records(torch.from_numpy(rec[s0:s1]), torch.from_numpy(st[s0:s1]), counts)
     ok_gather = bool(np.array_equal(g_rec.numpy(), rec) and np.array_equal(g_st.numpy(), st))
-    # predictive rows: compact index i owned by the rank whose month range holds it
+    # predictive rows: compact index i owned by the rank whose month range holds it; other
+    # ranks' rows hold the -0.0 record the device kernels write there (fm_ts.hip), so the SUM
+    # returns the owner's bits, signed zeros, infinities and NaNs included
     months = np.nonzero(st[:, 0])[0]
     pred_full = np.random.default_rng(9).standard_normal((1, len(months), 4))
+    pred_full[0, ::5, 0] = -0.0
+    pred_full[0, 1::5, 1] = 0.0
+    pred_full[0, 2::7, 2] = -np.inf
+    pred_full[0, 3::7, 0] = np.nan
     mine = (months >= s0) & (months < s1)
-    pred = np.where(mine[None, :, None], pred_full, 0.0)
+    pred = np.where(mine[None, :, None], pred_full, -0.0)
     pst = mine.astype(np.int32)[None, :]
     tp, ts = D.combine_predictive(torch.from_numpy(pred.copy()), torch.from_numpy(pst.copy()))
-    ok_pred = bool(np.array_equal(tp.numpy(), pred_full) and (ts.numpy() == 1).all())
+    ok_pred = bool(np.array_equal(tp.numpy().view(np.int64), pred_full.view(np.int64)) and (ts.numpy() == 1).all())
     mx = D.max_over_ranks(float(rank + 1), torch.device("cpu"))
     # gather_records_into (the call bench.py makes, into static global buffers): uneven
     # counts take the padded all_gather, equal counts all_gather_into_tensor
@@ -121,8 +127,9 @@ def test_combine_predictive_real_shard_outputs(world):
     (tests/golden/shard_pred.npz, written by tools/dump_shard_pred.py on the GPU: a ragged
     96-month panel in 3 shard_bounds ranges, each shard's time-series stage with its own
     moments).  The SUM all-reduce relies on every row of another shard's months being
-    exactly 0 (records and status); the combined result must equal the unsharded run bit for
-    bit on every fitted row, and the status words exactly."""
+    a zero record (-0.0 since round 6, +0.0 in fixtures dumped before; status 0); the combined
+    result must equal the unsharded run bit for bit on every fitted row, and the status words
+    exactly."""
     g = np.load(FIXTURE)
     for i in range(3):   # the fixture's premise: the shards' fitted rows are disjoint
         for j in range(i + 1, 3):

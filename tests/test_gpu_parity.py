@@ -1200,38 +1200,6 @@ def test_pipeline_headline_panel_full_size(E):
     _compare_with_oracle(gres, names, model_cols, ref, summ, roll, pred, pst, psumm)
 
 
-def test_pred_summary_in_launch_bit_identical(E):
-    """The predictive records' FM summary computed inside fm_ts_fused (world-1 runs, psum_*:
-    three workgroups per problem wait for its rolling workgroups) equals the separate fm_ts_fused launch on the records
-    (summarize_predictive) bit for bit: means, NW standard errors, t-stats, counts and the
-    compacted month index; repeated launches (the arrival counters reset themselves), a
-    problem with no fitted month, and a series with unfitted months inside."""
-    import torch
-    from fmcore import lewellen as LW
-    panel = E.panel_synthetic(420, 300, 5)
-    cfg = LW.PipelineConfig()
-    res, _, _, _, _ = LW.local_stage(panel, cfg, LW.table2_models())
-    st = res.status.clone()
-    st[:, 0] = 0                 # problem 0: nothing fitted
-    st[7:11, 2] = 0              # unfitted months inside problem 2's series
-    g = E.FMResult(problems=res.problems, rec=res.rec, status=st, pmax=res.pmax, moments=res.moments,
-                   mom_stride=res.mom_stride)
-    for _ in range(3):
-        ix, summ, roll, pred, pst, ps = LW.time_series_stage(g, cfg, moments=res.moments, pred_summary=True)
-        psumm, pix = ps
-        ref, rix = E.summarize_predictive(pred, pst, cfg.nw_lags)
-        torch.cuda.synchronize()
-        for f in ("mean", "se", "tstat", "nobs"):
-            assert _same(getattr(psumm, f).cpu().numpy(), getattr(ref, f).cpu().numpy()), f
-        cnt = pix.count.cpu().numpy()
-        assert np.array_equal(cnt, rix.count.cpu().numpy())
-        assert cnt[0] == 0 and np.isnan(psumm.mean[0].cpu().numpy()).all()
-        a, b = pix.idx.cpu().numpy(), rix.idx.cpu().numpy()
-        for k in range(len(cnt)):
-            assert np.array_equal(a[k, :cnt[k]], b[k, :cnt[k]]), k
-    assert int(E._psum_ctr(g.rec.device, len(res.problems)).abs().sum()) == 0
-
-
 def test_time_series_stage_gathered_c5_length(E):
     """C5's time-series stage at gathered length: every rank runs it on the full 100,000-month
     series of 11 problems (reference src/regressions.py:78-131, calc_Lewellen_2014.py:926).

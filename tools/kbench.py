@@ -28,8 +28,6 @@ def child():
 
     if os.environ.get("KB_PLANES") == "1":   # the split panel (fm_split_planes)
         E.split_planes(panel)
-    if os.environ.get("KB_PSUM") == "1":   # the predictive summary inside the time-series launch
-        LW.PRED_SUMMARY_IN_LAUNCH = True
     cfg = LW.PipelineConfig()
     for _ in range(3):
         LW.run_pipeline(panel, cfg)
@@ -54,7 +52,7 @@ def main():
             continue
         d = json.loads(line[0][3:])
         tag = os.path.basename(os.path.dirname(lib)) + (f"[chunk {os.environ['KB_CHUNK']}]" if os.environ.get("KB_CHUNK") else "")
-        tag += "".join(f"[{k}={os.environ[k]}]" for k in ("KB_POLICY", "KB_PLANES", "KB_PSUM", "KB_SLOTS") if os.environ.get(k))
+        tag += "".join(f"[{k}={os.environ[k]}]" for k in ("KB_POLICY", "KB_PLANES", "KB_SLOTS") if os.environ.get(k))
         print(tag, " ".join(f"{k}={v * 1e3:.1f}us" for k, v in d.items()), flush=True)
 
 
