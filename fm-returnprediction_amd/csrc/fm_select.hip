@@ -1493,56 +1493,71 @@ struct PairHkSmem {
     int okv[2];
 };
 
-// Values at ranks ra <= rb (rb <= ra + 1) of one tail's candidates L1 ++ L2 (c <= 64 R);
-// tail 1 holds complemented keys (ranks from the top).  false: cannot decide (never expected).
+// Values at ranks ra <= rb (rb <= ra + 1) of one tail's candidates L1 ++ L2 (c <= 64 R,
+// (key << 32 | row) each); tail 1 holds complemented keys (ranks from the top).  Only the
+// 32-bit keys are sorted (wave_sort32: a DPP exchange, min, max and lane-mask select per
+// register and stage); the keys at the two ranks are read back by readlane, and when each of
+// them belongs to exactly one candidate its row is found in the UNSORTED list by one ballot
+// per register, so the rows never travel through the sort.  When high words tie at the
+// target ranks, every tied candidate's full value is gathered and those are sorted (rare).
+// (Round 5 sorted the 64-bit (key, row) words: about 650 VALU per wave for R = 2 against
+// about 230 here.)  false: cannot decide (never expected).
 template <int R>
 __device__ __forceinline__ bool pick_hk(uint64_t* L1, int c1, const uint64_t* L2, int c2, int ra, int rb, int tail,
                                         const double* col, double& va, double& vb) {
     const int lane = lane_id();
     const int c = c1 + c2;
-    uint64_t v[R];
+    uint32_t key[R], row[R], sk[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int e = lane + WAVE * r;
-        v[r] = e < c1 ? L1[e] : (e < c ? L2[e - c1] : SENT);
+        const uint64_t x = e < c1 ? L1[e] : (e < c ? L2[e - c1] : SENT);
+        key[r] = (uint32_t)(x >> 32);   // padding: 0xFFFFFFFF, above every candidate key (<= HK_MAX)
+        row[r] = (uint32_t)x;
+        sk[r] = key[r];
     }
-    wave_sort<R>(v);
-    auto at = [&](int e) -> uint64_t {
-        const int q = e >> 6, l = e & 63;
-        uint64_t x = readlane_u64(v[0], l);
-        static_for<1, R>([&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            const uint64_t t = readlane_u64(v[r], l);
-            x = q == r ? t : x;
-        });
-        return x;
-    };
-    const uint64_t ea = at(ra), eb = at(rb);
-    const uint32_t Ka = (uint32_t)(ea >> 32), Kb = (uint32_t)(eb >> 32);
+    wave_sort32<R>(sk);
+    const uint32_t Ka = wave_at_u32<R>(sk, ra), Kb = wave_at_u32<R>(sk, rb);
     int p0 = 0, m = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const uint32_t k = (uint32_t)(v[r] >> 32);
-        const bool real = v[r] != SENT;
-        p0 += (int)__popcll(__ballot(real && k < Ka));
-        m += (int)__popcll(__ballot(real && k >= Ka && k <= Kb));
+        p0 += (int)__popcll(__ballot(key[r] < Ka));
+        m += (int)__popcll(__ballot(key[r] >= Ka && key[r] <= Kb));
     }
-    if (m == rb - ra + 1 && (ra == rb || Ka != Kb)) {   // distinct high words: two gathers
-        va = col[(uint32_t)ea];
-        vb = col[(uint32_t)eb];
+    if (m == rb - ra + 1 && (ra == rb || Ka != Kb)) {
+        // distinct high words at the target ranks: each key names one candidate
+        auto row_of = [&](uint32_t K) -> uint32_t {
+            uint32_t rw = 0;
+            bool found = false;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint64_t mk = __ballot(key[r] == K);
+                if (!found && mk != 0ull) {
+                    rw = (uint32_t)__builtin_amdgcn_readlane((int)row[r], (int)__builtin_ctzll(mk));
+                    found = true;
+                }
+            }
+            return rw;
+        };
+        const uint32_t rwa = row_of(Ka), rwb = ra == rb ? rwa : row_of(Kb);
+        va = col[rwa];
+        vb = col[rwb];
         return true;
     }
-    // high words tie at the target ranks: full keys of the tied candidates [p0, p0 + m),
-    // sorted in this wave's own (already loaded) list space
+    // high words tie at the target ranks: the full values of the candidates whose keys lie in
+    // [Ka, Kb] (ranks p0 .. p0 + m - 1) into this wave's own (already loaded) list space
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    int base = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int e = lane + WAVE * r;
-        if (e >= p0 && e < p0 + m) {
-            const double x = col[(uint32_t)v[r]];
-            L1[e - p0] = tail == 0 ? dkey(x) : ~dkey(x);
+        const bool in = key[r] >= Ka && key[r] <= Kb;
+        const uint64_t mk = __ballot(in);
+        if (in) {
+            const double x = col[row[r]];
+            L1[base + mask_rank(mk)] = tail == 0 ? dkey(x) : ~dkey(x);
         }
+        base += (int)__popcll(mk);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1745,7 +1760,8 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
                 const double* col = a.cols + (int64_t)c_cur * a.col_stride + a.seg_off[s_cur];
                 const int ra = t == 0 ? i0 : n - 1 - j1, rb = t == 0 ? j0 : n - 1 - i1;
                 double va = NAN, vb = NAN;
-                if (cc <= 2 * WAVE) good = pick_hk<2>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, t, col, va, vb);
+                if (cc <= WAVE) good = pick_hk<1>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, t, col, va, vb);
+                else if (cc <= 2 * WAVE) good = pick_hk<2>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, t, col, va, vb);
                 else good = pick_hk<4>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, t, col, va, vb);
                 // tail 1: ra / rb count from the top: va is the value at rank j1, vb at i1
                 if (lane == 0) sm.res[h] = t == 0 ? qlerp(va, vb, g0, mode) : qlerp(vb, va, g1, mode);

@@ -333,22 +333,54 @@ __device__ __forceinline__ void wave_sort_f64(double (&v)[R]) {
     if constexpr (K < WAVE * R) wave_sort_f64<R, K * 2>(v);
 }
 
-template <int K, int J>
-__device__ __forceinline__ void bitonic_u32_stages(uint32_t& v) {
-    uint32_t p0, p1;
-    xor_pair_u32<J>(v, p0, p1);
-    const uint32_t mn = p0 < p1 ? p0 : p1, mx = p0 < p1 ? p1 : p0;
-    v = cnd_u32(lane_mask<bitonic_min_mask<K, J, 0>()>(), mx, mn);
-    if constexpr (J > 1) bitonic_u32_stages<K, J / 2>(v);
+template <int R, int K, int J>
+__device__ __forceinline__ void bitonic_u32_stages(uint32_t (&v)[R]) {
+    if constexpr (J >= WAVE) {   // register-local: the role depends on r only
+        constexpr int rj = J / WAVE;
+        static_for<0, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            if constexpr ((r & rj) == 0) {
+                constexpr bool up = ((WAVE * r) & K) == 0;
+                const uint32_t a = v[r], b = v[r | rj];
+                const uint32_t mn = a < b ? a : b, mx = a < b ? b : a;
+                v[r] = up ? mn : mx;
+                v[r | rj] = up ? mx : mn;
+            }
+        });
+    } else {
+        static_for<0, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            uint32_t p0, p1;
+            xor_pair_u32<J>(v[r], p0, p1);
+            const uint32_t mn = p0 < p1 ? p0 : p1, mx = p0 < p1 ? p1 : p0;
+            v[r] = cnd_u32(lane_mask<bitonic_min_mask<K, J, r>()>(), mx, mn);
+        });
+    }
+    if constexpr (J > 1) bitonic_u32_stages<R, K, J / 2>(v);
 }
 
-// 32-bit keys, R == 1: one wave sorts its 64 lane values ascending (21 stages, one DPP /
-// permlane exchange each).
+// 32-bit keys: one wave sorts its 64 R values ascending (element e = lane + 64 r in register
+// r): one DPP / permlane exchange, a min, a max and a lane-mask select per register and
+// stage below 64, a register-local min / max at and above it (R = 1: 21 stages; R = 2: 28).
 template <int R, int K = 2>
 __device__ __forceinline__ void wave_sort32(uint32_t (&v)[R]) {
-    static_assert(R == 1, "wave_sort32: one register");
-    bitonic_u32_stages<K, K / 2>(v[0]);
-    if constexpr (K < WAVE) wave_sort32<R, K * 2>(v);
+    static_assert(R == 1 || R == 2 || R == 4, "wave_sort32: 1, 2 or 4 registers");
+    bitonic_u32_stages<R, K, K / 2>(v);
+    if constexpr (K < WAVE * R) wave_sort32<R, K * 2>(v);
+}
+
+// Element e (wave-uniform, < 64 R) of a wave-distributed u32 array: one readlane per register,
+// the register picked by scalar selects.
+template <int R>
+__device__ __forceinline__ uint32_t wave_at_u32(const uint32_t (&v)[R], int e) {
+    const int q = e >> 6, l = e & 63;
+    uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v[0], l);
+    static_for<1, R>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)v[r], l);
+        x = q == r ? t : x;
+    });
+    return x;
 }
 
 // Sort buf[0..c) (c <= 64*R) in place with one wave; entries c..64R-1 become SENT.
