@@ -66,6 +66,8 @@ def parse(argv=None):
     ap.add_argument("--no-planes", action="store_true",
                     help="keep the panel FP64-only (no high/low-word planes from fm_split_planes)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 per-rank shard at N=1")
+    ap.add_argument("--no-standardize", action="store_true",
+                    help="skip the C3 winsorize/standardize variant timed beside the headline")
     ap.add_argument("--no-headline", action="store_true", help="skip headline_weak at N>1")
     ap.add_argument("--dist-backend", default="nccl",
                     help="N>1 process group backend (nccl = RCCL; gloo only to rehearse on one GPU)")
@@ -323,6 +325,8 @@ def main():
         result["scaling_note"] = ("value at N>1 is the C5 workload; its N=1 point is the N=1 line's "
                                   "c5_rank_shard.rows_per_s (same per-rank shard), the headline's "
                                   "weak-scaled rate is headline_weak.value")
+    if world == 1 and workload == "headline" and not args.no_standardize:
+        result["standardize"] = standardize_stage(panel, args, E, LW, dev)
     if args.check and rank == 0 and world == 1 and workload == "headline":
         result["check"] = check_against_oracle(panel, gres, summ, args, LW)
     if rank == 0 and world == 1 and workload == "headline" and not args.no_cpu:
@@ -349,6 +353,35 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def standardize_stage(panel, args, E, LW, dev):
+    """BASELINE configs[2]'s "per-month winsorize/standardize" variant on the headline panel
+    (reported beside the headline, not part of `value`): PipelineConfig(standardize=True) --
+    the select kernels also return the clipped moments (the workgroup select path: moments
+    need every value), the Gram sees z-scores (shift = mean, inv_scale = 1/sd), degenerate
+    months are dropped -- replayed from a HIP graph and timed like the headline step."""
+    from fmcore.step import ShardedStep
+    cfg = LW.PipelineConfig(standardize=True)
+    step = ShardedStep(panel, cfg, LW.table2_models())
+    dt, out = timed_steps(step, args.steps, args.warmup, not args.no_graph, 1, dev)
+    ms = dt / args.steps * 1e3
+    rows = panel.nrows
+    timer = E.KernelTimer()
+    E.LAST_LAUNCH.clear()
+    with timer:
+        step.eager()
+    torch.cuda.synchronize()
+    kms = {t: round(E.time_launch(t, 10), 4) for t in ("fm_select_cuts", "fm_universe", "fm_gram", "fm_solve")
+           if t in E.LAST_LAUNCH}
+    res = {"ms_per_step": ms, "rows_per_s": rows / (ms * 1e-3), "steps": args.steps, "kernel_ms": kms,
+           "whole_pass_frac": rows * B_ROW / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "note": "PipelineConfig(standardize=True) on the headline panel: winsorize + per-month z-scores "
+                   "(A9) -> the same universes / models / time series; HIP graph replay"}
+    del step, out
+    E.LAST_LAUNCH.clear()
+    torch.cuda.empty_cache()
+    return res
 
 
 def c5_shard_stage(args, E, LW, dev):

@@ -1649,17 +1649,26 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
         // invalid keys counted per lane from the wrap of the max's offset add (one add with
         // carry per value), one wave sum after the loop instead of a ballot per value
         int nbad = 0;
+        // values in pairs: the lane min / max are one v_min3 / v_max3 per two values.  (A
+        // second copy of this loop that range-tests only the last register -- the bench's
+        // 5,000-row months fill the others -- pushed the kernel to 128 VGPRs with spills.)
+        static_assert(VPH % 2 == 0, "pairs of registers");
 #pragma unroll
-        for (int v = 0; v < VPH; ++v) {
-            const uint32_t kk = v * 2 * WAVE < lim ? hkey(xk[v]) : HK_NONE;
-            xk[v] = kk;
-            kmn = min(kmn, kk);
-            uint32_t kx;   // kk + 0x1FFFFE: NaN / absent keys wrap below every valid one (carry set)
-            asm volatile("v_add_co_u32 %0, vcc, 0x1ffffe, %2\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
-                         : "=&v"(kx), "+v"(nbad)
-                         : "v"(kk)
-                         : "vcc");
-            kmx2 = max(kmx2, kx);
+        for (int v = 0; v < VPH; v += 2) {
+            uint32_t kk[2], kx[2];
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+                const int vv = v + d;
+                kk[d] = vv * 2 * WAVE < lim ? hkey(xk[vv]) : HK_NONE;
+                xk[vv] = kk[d];
+                // kk + 0x1FFFFE: NaN / absent keys wrap below every valid one (carry set)
+                asm volatile("v_add_co_u32 %0, vcc, 0x1ffffe, %2\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+                             : "=&v"(kx[d]), "+v"(nbad)
+                             : "v"(kk[d])
+                             : "vcc");
+            }
+            kmn = min(kmn, min(kk[0], kk[1]));
+            kmx2 = max(kmx2, max(kx[0], kx[1]));
             asm volatile("" : "+v"(kmn), "+v"(kmx2));
         }
         nh = VPH * WAVE - wave_sum(nbad);
