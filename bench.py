@@ -418,26 +418,38 @@ def c5_shard_stage(args, E, LW, dev):
                    mom_stride=res.mom_stride)
     cfg = LW.PipelineConfig()
 
-    def ts():
-        ix, summ, roll, pred, pst = LW.time_series_stage(g, cfg, moments=res.moments, seg_lo=lo, seg_hi=hi)
-        E.summarize_predictive(pred, pst, cfg.nw_lags)
+    from fmcore import dist as D
+    prange = D.problem_block(res.nprob, world8, rank8)
 
-    ts()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(3):
-        ts()
-    e1.record()
-    e1.synchronize()
-    tsm = e0.elapsed_time(e1) / 3
+    def ts(sharded):
+        # sharded (what ShardedStep runs at N = 8): this rank's problem block of the summaries,
+        # rolling means only where its own months' predictive records read them
+        ix, summ, roll, pred, pst = LW.time_series_stage(g, cfg, moments=res.moments, seg_lo=lo, seg_hi=hi,
+                                                         sum_range=prange if sharded else None,
+                                                         roll_own=sharded)
+        E.summarize_predictive(pred, pst, cfg.nw_lags, sum_range=prange if sharded else None)
+
+    tsm = {}
+    for sharded in (True, False):
+        ts(sharded)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            ts(sharded)
+        e1.record()
+        e1.synchronize()
+        tsm[sharded] = e0.elapsed_time(e1) / 3
     out_d = {"rows": rows, "months": T, "firms": N, "seed": C5_SEED, "steps": args.c5_steps,
              "ms_per_pass": ms, "rows_per_s": rows / (ms * 1e-3), "regressions_per_s": nfit / (ms * 1e-3),
              "whole_pass_frac": rows * B_ROW / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel_ms": kms,
-             "ms_ts_gathered_100k": tsm, "split_planes_ms": split_ms,
+             "ms_ts_gathered_100k": tsm[True], "ms_ts_gathered_100k_replicated": tsm[False],
+             "split_planes_ms": split_ms,
              "note": "fmcore.step.ShardedStep at world 1 (HIP graph replay, timed like the headline): the "
-                     "N=1 point of the c5 workload; ms_ts_gathered_100k = the time-series stage on the "
-                     "100,000-month series an 8-rank all-gather assembles (run replicated per rank)"}
+                     "N=1 point of the c5 workload; ms_ts_gathered_100k = rank 4's share of the time-series "
+                     "stage on the 100,000-month series an 8-rank all-gather assembles (its problem block's "
+                     "summaries, rolling means / predictive records of its own months; _replicated: the "
+                     "whole stage, as every rank ran it before round 6)"}
     del step, p, out, gres, res, rec_g, st_g, g
     E.LAST_LAUNCH.clear()
     torch.cuda.empty_cache()

@@ -314,22 +314,46 @@ constexpr int RCH = TT / RKMAX * RPT;     // 256 output rows per workgroup
 constexpr int RMAXW = 1024;
 constexpr int RSPAN = RCH + 128;          // staged rows (windows up to 129 here): 52 KB of LDS
 
+// First position of the ascending list ix[0..n) holding a value >= v (block-uniform).
+__device__ __forceinline__ int lower_bound_i32(const int32_t* ix, int n, int v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ix[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// own != 0 (fm_rolling_mean_own): only the rows [ra, rb) = [first fitted row of a month >=
+// m_lo, minus lag; first fitted row of a month >= m_hi) are needed; workgroups and per-thread
+// row blocks without such a row are skipped, the others compute exactly as in the full mode
+// (same row-to-thread map, so the same bits), and no NaN fill is written.
 __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t r_seg,
                                                      int64_t r_prob, const int32_t* idx,
                                                      const int32_t* count, int nseg, int kmax,
-                                                     int window, int minp, double* out) {
+                                                     int window, int minp, double* out, int own,
+                                                     int m_lo, int m_hi, int lag) {
     __shared__ double xs[RSPAN * RKS];
     const int p = blockIdx.y;
     const int c0 = blockIdx.x * RCH;
     const int cnt = count[p];
-    // rows past the fitted-month count have no month: NaN (never left uninitialised)
-    const int cend = c0 + RCH < nseg ? c0 + RCH : nseg;
-    for (int e = threadIdx.x; e < (cend - c0) * kmax; e += TT) {
-        const int i = c0 + e / kmax;
-        if (i >= cnt) out[((int64_t)p * nseg + i) * kmax + (e % kmax)] = NAN;
+    const int32_t* ix = idx + (int64_t)p * nseg;
+    int ra = 0, rb = cnt;
+    if (own) {
+        ra = lower_bound_i32(ix, cnt, m_lo) - lag;
+        ra = ra < 0 ? 0 : ra;
+        rb = lower_bound_i32(ix, cnt, m_hi);
+        if (c0 + RCH <= ra || c0 >= rb) return;   // block-uniform
+    } else {
+        // rows past the fitted-month count have no month: NaN (never left uninitialised)
+        const int cend = c0 + RCH < nseg ? c0 + RCH : nseg;
+        for (int e = threadIdx.x; e < (cend - c0) * kmax; e += TT) {
+            const int i = c0 + e / kmax;
+            if (i >= cnt) out[((int64_t)p * nseg + i) * kmax + (e % kmax)] = NAN;
+        }
     }
     if (c0 >= cnt) return;
-    const int32_t* ix = idx + (int64_t)p * nseg;
     const int lo = c0 - window + 1 < 0 ? 0 : c0 - window + 1;
     const int hi = c0 + RCH < cnt ? c0 + RCH : cnt;
     for (int e = threadIdx.x; e < (hi - lo) * kmax; e += TT) {
@@ -340,6 +364,7 @@ __global__ __launch_bounds__(TT) void rolling_kernel(const double* rec, int64_t 
     const int k = threadIdx.x % RKMAX, g = threadIdx.x / RKMAX;
     const int ib = c0 + g * RPT;
     if (k >= kmax || ib >= hi) return;
+    if (own && (ib + RPT <= ra || ib >= rb)) return;   // this thread's rows are not needed
     const int j0 = ib - window + 1 < 0 ? 0 : ib - window + 1;
     CSum sm;   // compensated: an outlier leaving the window leaves no ulp(outlier) behind
     int c = 0;
@@ -613,13 +638,31 @@ extern "C" int fm_rolling_mean(const double* rec, int64_t r_seg, int64_t r_prob,
     if (kmax <= RKMAX && window <= RSPAN - RCH + 1) {
         dim3 grid((nseg + RCH - 1) / RCH, nprob);
         hipLaunchKernelGGL(rolling_kernel, grid, dim3(TT), 0, (hipStream_t)stream, rec, r_seg, r_prob,
-                           idx, count, nseg, kmax, window, min_periods, out);
+                           idx, count, nseg, kmax, window, min_periods, out, 0, 0, 0, 0);
     } else {
         dim3 grid((nseg + WRCH - 1) / WRCH, nprob * kmax);
         hipLaunchKernelGGL(rolling_kernel_wide, grid, dim3(TT), 0, (hipStream_t)stream, rec, r_seg, r_prob,
                            idx, count, nseg, kmax, window, min_periods, out);
     }
     FM_CHECK_LAUNCH("fm_rolling_mean");
+    return FM_OK;
+}
+
+extern "C" int fm_rolling_mean_own(const double* rec, int64_t r_seg, int64_t r_prob,
+                                   const int32_t* idx, const int32_t* count, int32_t nseg,
+                                   int32_t nprob, int32_t kmax, int32_t window, int32_t min_periods,
+                                   int32_t seg_lo, int32_t seg_hi, int32_t lag, double* out,
+                                   void* stream) {
+    using namespace fm;
+    FM_REQUIRE(rec && idx && count && out, "fm_rolling_mean_own: null pointer");
+    FM_REQUIRE(window >= 1 && min_periods >= 0 && lag >= 0, "fm_rolling_mean_own: bad window / lag");
+    FM_REQUIRE(kmax <= RKMAX && window <= RSPAN - RCH + 1,
+               "fm_rolling_mean_own: kmax <= %d and window <= %d (the staged kernel)", RKMAX, RSPAN - RCH + 1);
+    if (nprob == 0 || nseg == 0 || kmax == 0) return FM_OK;
+    dim3 grid((nseg + RCH - 1) / RCH, nprob);
+    hipLaunchKernelGGL(rolling_kernel, grid, dim3(TT), 0, (hipStream_t)stream, rec, r_seg, r_prob, idx, count,
+                       nseg, kmax, window, min_periods, out, 1, seg_lo, seg_hi, lag);
+    FM_CHECK_LAUNCH("fm_rolling_mean_own");
     return FM_OK;
 }
 
@@ -824,6 +867,37 @@ __device__ void ts_rolling_wg(const fm_ts_args& a, int p, int chunk, const int* 
     const int r0 = chunk * RROWS;
     const int T = a.nseg, PM = a.pmax;
     const bool predictive = a.pred != nullptr;
+    if (a.roll_own && r0 < cnt) {
+        // a sharded rank rolls only the rows its predictive records read: [first fitted row of
+        // its months - lag, first fitted row past them)
+        auto lb = [&](int v) {
+            int lo = 0, hi = cnt;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (ixs[mid] < v) lo = mid + 1;
+                else hi = mid;
+            }
+            return lo;
+        };
+        int ra = lb(a.seg_lo) - (predictive ? a.lag : 0);
+        ra = ra < 0 ? 0 : ra;
+        const int rb = lb(a.seg_hi);
+        if (r0 + RROWS <= ra || r0 >= rb) {   // block-uniform: none of this chunk's rows needed
+            if (predictive) {
+                // the chunk's predictive records are still this rank's to write: -0.0 records of
+                // other ranks' months, NaN past the fitted count (status 0), as below
+                const int e1 = r0 + RROWS < T ? r0 + RROWS : T;
+                for (int i = r0 + tid; i < e1; i += FT) {
+                    double* o = a.pred + ((int64_t)p * T + i) * 4;
+                    const bool row = i < cnt;
+                    o[0] = o[1] = o[2] = row ? -0.0 : NAN;
+                    o[3] = row ? -0.0 : 0.0;
+                    a.pred_status[(int64_t)p * T + i] = 0;
+                }
+            }
+            return;
+        }
+    }
     {
         // rows of this chunk past the fitted-month count hold no month: NaN rolling means,
         // NaN predictive record, status 0 (the buffers are never left uninitialised)
@@ -1060,7 +1134,16 @@ __global__ __launch_bounds__(FT) void ts_fused_kernel(fm_ts_args a) {
         if (threadIdx.x == 0) a.count[p] = cnt;
     }
     if (bx < a.kmax) {
-        ts_summary_wg(a, p, bx, ixs, cnt, lds_d, wtot, dred);
+        if (a.sum_p_hi > 0 && (p < a.sum_p_lo || p >= a.sum_p_hi)) {   // block-uniform
+            // another rank's problem (sharded runs): -0.0 / 0 for the exact SUM-combine
+            if (threadIdx.x == 0) {
+                const int64_t o = (int64_t)p * a.kmax + bx;
+                a.mean[o] = a.se[o] = a.tstat[o] = -0.0;
+                a.nobs[o] = 0;
+            }
+        } else {
+            ts_summary_wg(a, p, bx, ixs, cnt, lds_d, wtot, dred);
+        }
     } else {
         ts_rolling_wg(a, p, bx - a.kmax, ixs, cnt, lds_d);
         FM_PROBE_AT(ts, 6);

@@ -72,6 +72,8 @@ class TsArgs(C.Structure):
         ("work", _p), ("window", _i32), ("min_periods", _i32), ("pmax", _i32), ("roll", _p),
         ("moments", _p), ("mom_stride", _i32), ("prob_k", _p), ("lag", _i32), ("seg_lo", _i32),
         ("seg_hi", _i32), ("pred", _p), ("pred_status", _p),
+        # month-sharded runs: problem range of the summaries, own-rows rolling (0 = off)
+        ("sum_p_lo", _i32), ("sum_p_hi", _i32), ("roll_own", _i32), ("pad_ts", _i32),
     ]
 
 
@@ -128,6 +130,8 @@ _SIGS = {
     "fm_ts_summary": (_i32, [_p, _i64, _i64, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
                              _p, _p]),
     "fm_rolling_mean": (_i32, [_p, _i64, _i64, _p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p]),
+    "fm_rolling_mean_own": (_i32, [_p, _i64, _i64, _p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                   _p, _p]),
     "fm_predictive": (_i32, [_p, _i32, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _p, _p,
                              _p]),
     "fm_ts_fused": (_i32, [C.POINTER(TsArgs), _p]),

@@ -5,9 +5,13 @@ rank owns a contiguous month range, balanced by row count, and never exchanges p
 The only exchanges:
   1. all-gather of the per-(month, problem) records {intercept, slopes, R2, N} and status
      (a few KB per month) before the time-series stage, which every rank then runs on the
-     full series (FM means, Newey-West, 120-month rolling windows: no halos needed);
-  2. a sum all-reduce of the predictive-slope records, each rank having filled the rows of
-     its own months from its local centered moments.
+     full series, each doing only its share: the FM means / Newey-West summaries of its
+     block of problems (problem_block) and the 120-month rolling means and predictive-slope
+     records of its own months (the gathered series supplies the window halo);
+  2. a SUM all-reduce of the predictive-slope records and the summaries (every entry has
+     exactly one owner; the others hold -0.0 / 0, so the sum is the owner's value bit for
+     bit, signed zeros included);
+  3. a SUM all-reduce of the predictive summaries (again one owner per problem).
 The helpers are device-agnostic so the same code runs under gloo on CPU in the tests.
 """
 from __future__ import annotations
@@ -75,16 +79,30 @@ def gather_records_into(rec, status, rec_out, status_out, counts=None, group=Non
     return rec_out, status_out
 
 
-def combine_predictive(pred, pst, group=None):
-    """Rows of other ranks' months are zero in `pred`/`pst`: a SUM all-reduce merges them
-    (each compact row has exactly one owner)."""
-    for t in (pred, pst):
+def problem_block(nprob, world, rank):
+    """Contiguous problem range [p0, p1) of a rank for the sharded FM summaries (blocks
+    differ in size by at most one; empty when there are more ranks than problems)."""
+    return (nprob * rank) // world, (nprob * (rank + 1)) // world
+
+
+def combine_sum(tensors, group=None):
+    """SUM all-reduce of each tensor in place.  Every entry has one owner rank; the others
+    hold -0.0 (floats) or 0 (integers), so the result is the owner's value bit for bit:
+    v + (-0.0) == v for every v, signed zeros, infinities and NaNs included, in any order."""
+    for t in tensors:
         if _host_staged(t, group):
             h = t.cpu()
             dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
             t.copy_(h)
         else:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return tensors
+
+
+def combine_predictive(pred, pst, group=None):
+    """Rows of other ranks' months are -0.0 records / status 0 in `pred`/`pst` (fm_ts.hip):
+    a SUM all-reduce merges them exactly (each compact row has exactly one owner)."""
+    combine_sum((pred, pst), group)
     return pred, pst
 
 

@@ -833,30 +833,56 @@ class Summary:
     nobs: torch.Tensor
 
 
-def ts_summary(rec, r_seg, r_prob, ix: TSIndex, nseg, nprob, kmax, nw_lags=4):
+def _sum_outputs(nprob, kmax, dev, sum_range):
+    """Summary output buffers; with a problem range (sharded runs) pre-filled with the -0.0 /
+    0 that the SUM-combine across ranks needs for the problems this rank does not summarize."""
+    if sum_range is None:
+        mean = torch.empty((nprob, kmax), dtype=torch.float64, device=dev)
+        se, ts = torch.empty_like(mean), torch.empty_like(mean)
+        nobs = torch.empty((nprob, kmax), dtype=torch.int32, device=dev)
+    else:
+        mean = torch.full((nprob, kmax), -0.0, dtype=torch.float64, device=dev)
+        se, ts = mean.clone(), mean.clone()
+        nobs = torch.zeros((nprob, kmax), dtype=torch.int32, device=dev)
+    return mean, se, ts, nobs
+
+
+def ts_summary(rec, r_seg, r_prob, ix: TSIndex, nseg, nprob, kmax, nw_lags=4, sum_range=None):
+    """FM means / NW standard errors of every (problem, coefficient).  ``sum_range`` = (p0, p1):
+    problems [p0, p1) only (pointer offsets into the same buffers), -0.0 / 0 elsewhere."""
     dev = rec.device
-    mean = torch.empty((nprob, kmax), dtype=torch.float64, device=dev)
-    se, ts = torch.empty_like(mean), torch.empty_like(mean)
-    nobs = torch.empty((nprob, kmax), dtype=torch.int32, device=dev)
-    # the series [nprob][kmax][nseg] and the long-series chunk partials (fm_hip.h)
-    work = torch.empty(nprob * kmax * (max(nseg, 1) + -(-nseg // 2048) * 28), dtype=torch.float64, device=dev)
-    _kcall("fm_ts_summary", "fm_ts_summary", rec.data_ptr(), r_seg, r_prob, ix.idx.data_ptr(), ix.count.data_ptr(),
-           nseg, nprob, kmax, nw_lags, mean.data_ptr(), se.data_ptr(), ts.data_ptr(), nobs.data_ptr(),
-           work.data_ptr(), _stream())
+    mean, se, ts, nobs = _sum_outputs(nprob, kmax, dev, sum_range)
+    p0, p1 = (0, nprob) if sum_range is None else sum_range
+    n = p1 - p0
+    if n <= 0:
+        return Summary(mean, se, ts, nobs)
+    # the series [n][kmax][nseg] and the long-series chunk partials (fm_hip.h)
+    work = torch.empty(n * kmax * (max(nseg, 1) + -(-nseg // 2048) * 28), dtype=torch.float64, device=dev)
+    _kcall("fm_ts_summary", "fm_ts_summary", rec.data_ptr() + 8 * p0 * r_prob, r_seg, r_prob,
+           ix.idx[p0].data_ptr(), ix.count[p0:].data_ptr(), nseg, n, kmax, nw_lags, mean[p0].data_ptr(),
+           se[p0].data_ptr(), ts[p0].data_ptr(), nobs[p0].data_ptr(), work.data_ptr(), _stream())
     return Summary(mean, se, ts, nobs)
 
 
-def summarize_result(res: FMResult, ix: TSIndex = None, nw_lags=4):
+def summarize_result(res: FMResult, ix: TSIndex = None, nw_lags=4, sum_range=None):
     ix = ix or compact_result(res)
     T, P, rs = res.rec.shape
-    return ts_summary(res.rec, P * rs, rs, ix, T, P, rs, nw_lags), ix
+    return ts_summary(res.rec, P * rs, rs, ix, T, P, rs, nw_lags, sum_range), ix
 
 
-def rolling_result(res: FMResult, ix: TSIndex, window=120, min_periods=60):
+def rolling_result(res: FMResult, ix: TSIndex, window=120, min_periods=60, own=None):
+    """Rolling means [P, T, pmax] of the fitted-month series.  ``own`` = (seg_lo, seg_hi, lag)
+    (sharded runs): only the rows a predictive stage of those months reads, the same bits
+    (fm_rolling_mean_own); other rows are left unwritten."""
     T, P, rs = res.rec.shape
     out = torch.empty((P, T, res.pmax), dtype=torch.float64, device=res.rec.device)
-    _kcall("fm_rolling_mean", "fm_rolling_mean", res.rec.data_ptr(), P * rs, rs, ix.idx.data_ptr(), ix.count.data_ptr(),
-           T, P, res.pmax, window, min_periods, out.data_ptr(), _stream())
+    if own is None:
+        _kcall("fm_rolling_mean", "fm_rolling_mean", res.rec.data_ptr(), P * rs, rs, ix.idx.data_ptr(),
+               ix.count.data_ptr(), T, P, res.pmax, window, min_periods, out.data_ptr(), _stream())
+    else:
+        _kcall("fm_rolling_mean", "fm_rolling_mean_own", res.rec.data_ptr(), P * rs, rs, ix.idx.data_ptr(),
+               ix.count.data_ptr(), T, P, res.pmax, window, min_periods, int(own[0]), int(own[1]), int(own[2]),
+               out.data_ptr(), _stream())
     return out
 
 
@@ -889,12 +915,20 @@ def predictive_result(res: FMResult, ix: TSIndex, roll, lag=1, seg_lo=0, seg_hi=
     return pred, pst
 
 
-def summarize_predictive(pred, pst, nw_lags=4):
+def summarize_predictive(pred, pst, nw_lags=4, sum_range=None):
+    """FM summary of the predictive records (slope, R^2, n).  ``sum_range`` (sharded runs):
+    problems [p0, p1) only, -0.0 / 0 elsewhere (combined across ranks by a SUM)."""
     P, T, _ = pred.shape
     if not ts_fused_fits(T):
-        ix = ts_compact(pst, 1, T, T, P)
-        return ts_summary(pred, 4, T * 4, ix, T, P, 3, nw_lags), ix
-    ix, summ, _, _, _ = ts_fused(pred, 4, T * 4, pst, 1, T, T, P, 3, nw_lags, tag="fm_ts_fused[pred]")
+        p0, p1 = (0, P) if sum_range is None else sum_range
+        ix = TSIndex(torch.empty((P, T), dtype=torch.int32, device=pred.device),
+                     torch.zeros(P, dtype=torch.int32, device=pred.device))
+        if p1 > p0:
+            _kcall("fm_ts_compact", "fm_ts_compact", pst[p0].data_ptr(), 1, T, T, p1 - p0, ix.idx[p0].data_ptr(),
+                   ix.count[p0:].data_ptr(), _stream())
+        return ts_summary(pred, 4, T * 4, ix, T, P, 3, nw_lags, sum_range), ix
+    ix, summ, _, _, _ = ts_fused(pred, 4, T * 4, pst, 1, T, T, P, 3, nw_lags, tag="fm_ts_fused[pred]",
+                                 sum_range=sum_range)
     return summ, ix
 
 
@@ -907,10 +941,13 @@ def ts_fused_fits(nseg, pmax=0, window=None, lag=1, predictive=False):
 
 def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_lags=4,
              window=None, min_periods=None, pmax=None, moments=None, mom_stride=0, prob_k=None,
-             lag=1, seg_lo=0, seg_hi=None, predictive=False, tag="fm_ts_fused"):
+             lag=1, seg_lo=0, seg_hi=None, predictive=False, tag="fm_ts_fused", sum_range=None,
+             roll_own=False):
     """The whole time-series stage in one launch (fm_ts_fused): TSIndex, Summary and, when
     ``window`` is given, the rolling means [P, T, pmax]; with ``predictive`` also the
-    predictive records [P, T, 4] and status [P, T].  Returns (ix, summ, roll, pred, pst)."""
+    predictive records [P, T, 4] and status [P, T].  Returns (ix, summ, roll, pred, pst).
+    Sharded runs: ``sum_range`` = (p0, p1) summarizes problems [p0, p1) only (-0.0 / 0
+    elsewhere), ``roll_own`` rolls only the rows the months [seg_lo, seg_hi) read."""
     dev = rec.device
     idx = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
     cnt = torch.empty(nprob, dtype=torch.int32, device=dev)
@@ -923,13 +960,21 @@ def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_la
     if predictive:
         pred = torch.empty((nprob, nseg, 4), dtype=torch.float64, device=dev)
         pst = torch.empty((nprob, nseg), dtype=torch.int32, device=dev)
+    # problem range of the summaries: (0, 0) = every problem; an empty range of a sharded rank
+    # (more ranks than problems) = (nprob, nprob): the kernel then summarizes none
+    sp_lo, sp_hi = 0, 0
+    if sum_range is not None:
+        sp_lo, sp_hi = int(sum_range[0]), int(sum_range[1])
+        if sp_hi <= sp_lo:
+            sp_lo = sp_hi = nprob
     ta = L.TsArgs(rec=rec.data_ptr(), r_seg=r_seg, r_prob=r_prob, status=status.data_ptr(), s_seg=s_seg,
                   s_prob=s_prob, nseg=nseg, nprob=nprob, kmax=kmax, nw_lags=nw_lags, idx=idx.data_ptr(),
                   count=cnt.data_ptr(), mean=mean.data_ptr(), se=se.data_ptr(), tstat=ts.data_ptr(),
                   nobs=nobs.data_ptr(), work=None, window=window or 0,
                   min_periods=min_periods or 0, pmax=pmax or 0, roll=_ptr(roll), moments=_ptr(moments),
                   mom_stride=mom_stride, prob_k=_ptr(prob_k), lag=lag, seg_lo=seg_lo,
-                  seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst))
+                  seg_hi=nseg if seg_hi is None else seg_hi, pred=_ptr(pred), pred_status=_ptr(pst),
+                  sum_p_lo=sp_lo, sum_p_hi=sp_hi, roll_own=int(bool(roll_own)))
     _kcall(tag, "fm_ts_fused", L.C.byref(ta), _stream())
     _remember(tag, "fm_ts_fused", ta, rec, status, idx, cnt, mean, se, ts, nobs, roll,
               moments, prob_k, pred, pst)
@@ -937,18 +982,24 @@ def ts_fused(rec, r_seg, r_prob, status, s_seg, s_prob, nseg, nprob, kmax, nw_la
 
 
 def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag=1, seg_lo=0,
-                       seg_hi=None, moments=None, rolling=True, predictive=True):
+                       seg_hi=None, moments=None, rolling=True, predictive=True, sum_range=None,
+                       roll_own=False):
     """compact_result + summarize_result + rolling_result + predictive_result in one launch.
-    Returns (ix, summ, roll, pred, pst)."""
+    Returns (ix, summ, roll, pred, pst).  Sharded runs (every rank on the gathered series):
+    ``sum_range`` = this rank's problems for the FM summaries, ``roll_own`` = rolling means only
+    where this rank's predictive records [seg_lo, seg_hi) read them."""
     T, P, rs = res.rec.shape
     mom = res.moments if moments is None else moments
     window = window if (rolling or predictive) else None
     if not ts_fused_fits(T, res.pmax, window, lag, predictive):
         ix = compact_result(res)
-        summ, _ = summarize_result(res, ix, nw_lags)
+        summ, _ = summarize_result(res, ix, nw_lags, sum_range)
         roll = pred = pst = None
         if window is not None:
-            roll = rolling_result(res, ix, window, min_periods)
+            own = None
+            if roll_own:
+                own = (seg_lo, T if seg_hi is None else seg_hi, lag if predictive else 0)
+            roll = rolling_result(res, ix, window, min_periods, own)
         if predictive:
             pred, pst = predictive_result(res, ix, roll, lag, seg_lo, seg_hi, moments)
         return ix, summ, roll, pred, pst
@@ -956,7 +1007,8 @@ def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag
     return ts_fused(res.rec, P * rs, rs, res.status, P, 1, T, P, rs, nw_lags,
                     window=window, min_periods=min_periods,
                     pmax=res.pmax, moments=mom if predictive else None, mom_stride=res.mom_stride,
-                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive)
+                    prob_k=pk, lag=lag, seg_lo=seg_lo, seg_hi=seg_hi, predictive=predictive,
+                    sum_range=sum_range, roll_own=roll_own)
 
 
 def forecast(panel: DevicePanel, coef, cols=None):

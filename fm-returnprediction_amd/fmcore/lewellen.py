@@ -163,12 +163,17 @@ def local_stage(panel: E.DevicePanel, cfg: PipelineConfig, model_cols, y="retx")
     return res, names, cuts, level, bp
 
 
-def time_series_stage(res: E.FMResult, cfg: PipelineConfig, moments=None, seg_lo=0, seg_hi=None):
+def time_series_stage(res: E.FMResult, cfg: PipelineConfig, moments=None, seg_lo=0, seg_hi=None,
+                      sum_range=None, roll_own=False):
     """One launch (fm_ts_fused): compaction, FM summaries, rolling means, predictive slopes.
-    Their FM summary follows in summarize_predictive.  Returns (ix, summ, roll, pred, pst)."""
+    Their FM summary follows in summarize_predictive.  Returns (ix, summ, roll, pred, pst).
+    Month-sharded ranks pass their problem block (``sum_range``) and ``roll_own`` (rolling
+    means only where their own months' predictive records read them); the summaries are then
+    SUM-combined across ranks (fmcore.step.ShardedStep)."""
     return E.time_series_result(
         res, cfg.nw_lags, cfg.window, cfg.min_periods, cfg.lag, seg_lo=seg_lo, seg_hi=seg_hi,
-        moments=moments, rolling=cfg.forecasts or cfg.fig1, predictive=cfg.forecasts)
+        moments=moments, rolling=cfg.forecasts or cfg.fig1, predictive=cfg.forecasts,
+        sum_range=sum_range, roll_own=roll_own)
 
 
 def run_pipeline(panel: E.DevicePanel, cfg: PipelineConfig = None, model_cols=None, y="retx"):

@@ -1,13 +1,16 @@
 """One step of the month-sharded full Fama-MacBeth pass (what bench.py times).
 
-A step is three device phases with the two exchanges of SURVEY.md §8(e) between them:
+A step is three device phases with the exchanges of SURVEY.md §8(e) between them:
 
   phase_local   cuts, universes, batched Gram + solve of this rank's months
   exchange 1    all-gather of the monthly records into static global buffers
-  phase_ts      time-series stage on the full series (FM means, NW, rolling means, the
-                predictive records of this rank's months)
-  exchange 2    SUM all-reduce of the predictive records (each row has one owner)
-  phase_pred    FM summary of the predictive slopes
+  phase_ts      time-series stage on the gathered series, this rank's share only: the FM
+                means / NW of its problem block (dist.problem_block), the rolling means and
+                predictive records of its own months
+  exchange 2    SUM all-reduce of the predictive records and the summaries (one owner each;
+                the others hold -0.0 / 0)
+  phase_pred    FM summary of the predictive slopes of its problem block
+  exchange 3    SUM all-reduce of the predictive summaries
 
 Without exchanges (world size 1, no process group) the whole step can be replayed from ONE
 HIP graph; otherwise each phase is its own graph (static buffers), with the collectives
@@ -25,7 +28,8 @@ from . import lewellen as LW
 
 class ShardedStep:
     def __init__(self, panel: E.DevicePanel, cfg: LW.PipelineConfig, model_cols, world=1, rank=0,
-                 seg_lo=0, seg_hi=None, global_months=None, counts=None, group=None, exchange=None):
+                 seg_lo=0, seg_hi=None, global_months=None, counts=None, group=None, exchange=None,
+                 shard_ts=None):
         self.panel, self.cfg, self.model_cols = panel, cfg, model_cols
         self.world, self.rank, self.group = world, rank, group
         self.seg_lo = seg_lo
@@ -41,9 +45,15 @@ class ShardedStep:
         self.exchange = world > 1 if exchange is None else bool(exchange)
         if world > 1 and not self.exchange:
             raise ValueError("a sharded step (world > 1) needs its exchanges")
+        # the time-series stage split across the ranks (problem blocks, own-month rolling);
+        # False: every rank runs all of it on the gathered series (round-5 behaviour)
+        self.shard_ts = self.exchange if shard_ts is None else bool(shard_ts) and self.exchange
         self.rec_g = self.st_g = None
         self.graphs = None
         self._out = None
+
+    def _sum_range(self, nprob):
+        return D.problem_block(nprob, self.world, self.rank) if self.shard_ts else None
 
     # ---- phases ------------------------------------------------------------------------
     def phase_local(self):
@@ -66,18 +76,32 @@ class ShardedStep:
             gres = E.FMResult(problems=res.problems, rec=self.rec_g, status=self.st_g, pmax=res.pmax,
                               moments=res.moments, mom_stride=res.mom_stride)
         ix, summ, roll, pred, pst = LW.time_series_stage(gres, self.cfg, moments=res.moments,
-                                                         seg_lo=self.seg_lo, seg_hi=self.seg_hi)
+                                                         seg_lo=self.seg_lo, seg_hi=self.seg_hi,
+                                                         sum_range=self._sum_range(res.nprob),
+                                                         roll_own=self.shard_ts)
+        self._summ = summ
         return gres, summ, pred, pst
 
     def exchange_pred(self, pred, pst):
-        if self.exchange and pred is not None:
-            D.combine_predictive(pred, pst, self.group)
+        if not self.exchange:
+            return
+        ts = []
+        if pred is not None:
+            ts += [pred, pst]
+        if self.shard_ts:
+            sm = self._summ
+            ts += [sm.mean, sm.se, sm.tstat, sm.nobs]
+        D.combine_sum(ts, self.group)
 
     def phase_pred(self, pred, pst):
         if pred is None:
             return None
-        psumm, _ = E.summarize_predictive(pred, pst, self.cfg.nw_lags)
+        psumm, _ = E.summarize_predictive(pred, pst, self.cfg.nw_lags, sum_range=self._sum_range(pred.shape[0]))
         return psumm
+
+    def exchange_psumm(self, psumm):
+        if self.shard_ts and psumm is not None:
+            D.combine_sum((psumm.mean, psumm.se, psumm.tstat, psumm.nobs), self.group)
 
     # ---- whole step --------------------------------------------------------------------
     def eager(self):
@@ -86,7 +110,9 @@ class ShardedStep:
         self.exchange_records(res)
         gres, summ, pred, pst = self.phase_ts(res)
         self.exchange_pred(pred, pst)
-        return gres, summ, self.phase_pred(pred, pst)
+        psumm = self.phase_pred(pred, pst)
+        self.exchange_psumm(psumm)
+        return gres, summ, psumm
 
     def capture(self):
         """Capture the phases as HIP graphs.  Every host-side cache (chunk plans, model
@@ -121,7 +147,9 @@ class ShardedStep:
             gc = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gc):
                 psumm = self.phase_pred(pred, pst)
+            self.exchange_psumm(psumm)
         self.graphs = (ga, gb, gc)
+        self._psumm = psumm
         self._static = (res, pred, pst)
         self._out = (gres, summ, psumm)
 
@@ -139,4 +167,5 @@ class ShardedStep:
         self.exchange_pred(pred, pst)
         if gc is not None:
             gc.replay()
+            self.exchange_psumm(self._psumm)
         return self._out

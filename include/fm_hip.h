@@ -328,6 +328,15 @@ int fm_rolling_mean(const double* rec, int64_t r_seg, int64_t r_prob, const int3
                     const int32_t* count, int32_t nseg, int32_t nprob, int32_t kmax,
                     int32_t window, int32_t min_periods, double* out, void* stream);
 
+/* fm_rolling_mean for a month-sharded rank: only the output rows a predictive stage of months
+ * [seg_lo, seg_hi) reads (the fitted rows of those months and the `lag` rows before the
+ * first), computed exactly as fm_rolling_mean computes them (same bits); other rows of `out`
+ * are left unwritten (the per-thread row blocks that hold no such row are skipped). */
+int fm_rolling_mean_own(const double* rec, int64_t r_seg, int64_t r_prob, const int32_t* idx,
+                        const int32_t* count, int32_t nseg, int32_t nprob, int32_t kmax,
+                        int32_t window, int32_t min_periods, int32_t seg_lo, int32_t seg_hi,
+                        int32_t lag, double* out, void* stream);
+
 int fm_predictive(const double* moments, int32_t mom_stride, int32_t nseg, int32_t nprob,
                   const int32_t* prob_k, const int32_t* idx, const int32_t* count,
                   const double* rolling, int32_t pmax, int32_t lag, int32_t seg_lo,
@@ -360,6 +369,20 @@ typedef struct fm_ts_args {
     int32_t lag, seg_lo, seg_hi;
     double* pred;                 /* [nprob][nseg][4] or NULL */
     uint32_t* pred_status;        /* [nprob][nseg] */
+    /* Month-sharded runs (zero-initialised = off; every rank runs the stage on the gathered
+     * series, each doing only its share):
+     *   sum_p_hi > 0: the FM summaries (mean, se, tstat, nobs) of problems [sum_p_lo,
+     *     sum_p_hi) only; the other problems' summaries are written as -0.0 / 0, so a SUM
+     *     all-reduce over the ranks returns every problem's summary bit for bit;
+     *   roll_own != 0: rolling means only in the rolling workgroups whose rows hold a fitted
+     *     month in [seg_lo, seg_hi) or one of the `lag` rows before the first such row (the
+     *     rows this rank's predictive records read); the other workgroups write no rolling
+     *     means (those roll rows are left unwritten) but still their predictive records
+     *     (-0.0 / status 0 for other ranks' months).  Computed rows are bit-identical to a
+     *     full run's. */
+    int32_t sum_p_lo, sum_p_hi;
+    int32_t roll_own;
+    int32_t pad_ts;
 } fm_ts_args;
 
 /* LDS bytes the fused launch stages per workgroup; it must not exceed FM_TS_FUSED_MAX_LDS

@@ -1233,6 +1233,59 @@ def test_time_series_stage_gathered_c5_length(E):
         assert rows.min() >= rank * Tl - 1 and rows.max() < (rank + 1) * Tl, k
 
 
+@pytest.mark.parametrize("path", ["fused", "per_stage"])
+def test_sharded_time_series_stage_bit_identical(E, path):
+    """The time-series stage split over W month-sharded ranks (ShardedStep, round 6): each rank
+    summarizes its problem block (dist.problem_block; -0.0 / 0 for the others), rolls only the
+    rows its own months' predictive records read, writes -0.0 records for other ranks' months;
+    the SUM of the ranks' outputs (what the RCCL all-reduces return) equals the unsharded stage
+    bit for bit, signed zeros included: summaries, predictive records and status, and the
+    predictive summaries computed per problem block on the combined records.  Both the fused
+    launch (a short gathered series) and the per-stage kernels (a 100,000-month series, C5's
+    gathered length) are covered; W = 3 uneven month ranges."""
+    import torch
+    from fmcore import dist as D
+    from fmcore import lewellen as LW
+    Tl, tile, W = (200, 4, 3) if path == "fused" else (12500, 8, 3)
+    panel = E.panel_synthetic(Tl, 120 if path == "fused" else 200, 31, month0=0)
+    cfg = LW.PipelineConfig()
+    res, _, _, _, _ = LW.local_stage(panel, cfg, LW.table2_models())
+    rec = res.rec.repeat(tile, 1, 1).contiguous()
+    st = res.status.repeat(tile, 1).contiguous()
+    st[5, :] = 0
+    rec[5, :, :] = float("nan")
+    T, P = st.shape
+    mom = res.moments.repeat(tile, 1, 1).contiguous()
+    g = E.FMResult(problems=res.problems, rec=rec, status=st, pmax=res.pmax, moments=mom,
+                   mom_stride=res.mom_stride)
+    assert E.ts_fused_fits(T, res.pmax, cfg.window, cfg.lag, predictive=True) == (path == "fused")
+    ix, summ, roll, pred, pst = LW.time_series_stage(g, cfg, moments=mom, seg_lo=0, seg_hi=T)
+    psumm, _ = E.summarize_predictive(pred, pst, cfg.nw_lags)
+    bounds = D.shard_bounds(np.full(T, 1), W)
+    acc = None
+    outs = []
+    for r, (s0, s1) in enumerate(bounds):
+        blk = D.problem_block(P, W, r)
+        _, sm, _, pr, ps = LW.time_series_stage(g, cfg, moments=mom[s0:s1], seg_lo=s0, seg_hi=s1,
+                                                sum_range=blk, roll_own=True)
+        parts = [pr, ps, sm.mean, sm.se, sm.tstat, sm.nobs]
+        acc = [t.clone() for t in parts] if acc is None else [a + t for a, t in zip(acc, parts)]
+        outs.append(blk)
+    cpred, cpst = acc[0], acc[1]
+    pacc = None
+    for r in range(W):
+        ps_r, _ = E.summarize_predictive(cpred, cpst, cfg.nw_lags, sum_range=outs[r])
+        parts = [ps_r.mean, ps_r.se, ps_r.tstat, ps_r.nobs]
+        pacc = [t.clone() for t in parts] if pacc is None else [a + t for a, t in zip(pacc, parts)]
+    torch.cuda.synchronize()
+    full = [pred, pst, summ.mean, summ.se, summ.tstat, summ.nobs]
+    names = ["pred", "pst", "mean", "se", "tstat", "nobs"]
+    for nm, a, b in zip(names, acc, full):
+        assert _same(a.cpu().numpy(), b.cpu().numpy()), nm
+    for nm, a, b in zip(["pmean", "pse", "ptstat", "pnobs"], pacc, [psumm.mean, psumm.se, psumm.tstat, psumm.nobs]):
+        assert _same(a.cpu().numpy(), b.cpu().numpy()), nm
+
+
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
 def test_pipeline_single_model_configs(E, cfg):
     """C1 (Model 1, K=3) and C2 (Model 2, K=7) alone, 3 universes, no Figure 1."""
