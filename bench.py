@@ -64,7 +64,7 @@ def parse(argv=None):
     ap.add_argument("--check", action="store_true", help="verify one step against the oracle")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
     ap.add_argument("--no-planes", action="store_true",
-                    help="keep the panel FP64-only (no high/low-word planes from fm_split_planes)")
+                    help="generate the panel as FP64 columns (default: the split high/low-word planes only)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 per-rank shard at N=1")
     ap.add_argument("--no-standardize", action="store_true",
                     help="skip the C3 winsorize/standardize variant timed beside the headline")
@@ -161,25 +161,23 @@ def timed_steps(step, steps, warmup, graph, world, dev):
     return dt, out
 
 
-def split_ingest(panel, E, planes=True):
-    """The panel's ingest-time layout pass (outside the timed step): the FP64 columns split
-    into their high / low 32-bit planes (fm_split_planes), which the selects and the Gram read.
-    Returns its device time in ms (HIP events), reported beside the step, never in it."""
-    if not planes:
-        return None
+def gen_panel(T, N, seed, month0, dev, E, planes=True):
+    """The rank's panel generated in HBM (outside the timed step, like a real panel's ingest):
+    by default in the split layout only -- fm_gen_panel_planes writes the values' high / low
+    32-bit planes, which the selects (high plane) and the Gram (both) read; no FP64 columns, no
+    separate layout pass.  --no-planes: FP64 columns only.  Returns (panel, device ms)."""
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    E.split_planes(panel)
+    panel = E.panel_synthetic(T, N, seed, month0=month0, device=dev, layout="planes" if planes else "f64")
     e1.record()
     e1.synchronize()
-    return e0.elapsed_time(e1)
+    return panel, e0.elapsed_time(e1)
 
 
 def make_step(T_loc, N, seed, world, rank, dev, E, LW, planes=True):
     from fmcore.step import ShardedStep
-    panel = E.panel_synthetic(T_loc, N, seed, month0=rank * T_loc, device=dev)
-    panel.ingest_ms = split_ingest(panel, E, planes)
+    panel, panel.gen_ms = gen_panel(T_loc, N, seed, rank * T_loc, dev, E, planes)
     T_glob = T_loc * world
     # one Gram plan for every rank, made from the GLOBAL panel's sizes and cut in global row
     # space, so a month's partial sums (and their order) do not depend on the rank count
@@ -317,9 +315,10 @@ def main():
         "lib_sha16": _lib_sha(),
         "kernel_ms_eager_events": {k: round(v, 4) for k, v in kern.items()},
         "graph": not args.no_graph,
-        "ingest": {"split_planes_ms": panel.ingest_ms,
-                   "note": "layout pass at ingest (FP64 columns -> high/low 32-bit planes, fm_split_planes), "
-                           "outside the timed step like the panel's generation"},
+        "ingest": {"gen_ms": panel.gen_ms, "layout": "planes" if panel.cols is None else "f64",
+                   "panel_hbm_bytes": _panel_bytes(panel),
+                   "note": "the panel generated in HBM directly in its layout (fm_gen_panel_planes: high / low "
+                           "32-bit planes, no FP64 columns, no separate layout pass), outside the timed step"},
     }
     if world > 1:
         result["scaling_note"] = ("value at N>1 is the C5 workload; its N=1 point is the N=1 line's "
@@ -394,8 +393,7 @@ def c5_shard_stage(args, E, LW, dev):
     which every rank of the 8-GPU run executes replicated."""
     T, N, world8, rank8 = args.c5_months, args.c5_firms, 8, 4
     from fmcore.step import ShardedStep
-    p = E.panel_synthetic(T, N, C5_SEED, month0=rank8 * T, device=dev)
-    split_ms = split_ingest(p, E, not args.no_planes)
+    p, gen_ms = gen_panel(T, N, C5_SEED, rank8 * T, dev, E, not args.no_planes)
     step = ShardedStep(p, LW.PipelineConfig(), LW.table2_models(), seg_lo=rank8 * T, seg_hi=(rank8 + 1) * T)
     dt, out = timed_steps(step, args.c5_steps, 1, not args.no_graph, 1, dev)
     ms = dt / args.c5_steps * 1e3
@@ -444,7 +442,7 @@ def c5_shard_stage(args, E, LW, dev):
              "ms_per_pass": ms, "rows_per_s": rows / (ms * 1e-3), "regressions_per_s": nfit / (ms * 1e-3),
              "whole_pass_frac": rows * B_ROW / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel_ms": kms,
              "ms_ts_gathered_100k": tsm[True], "ms_ts_gathered_100k_replicated": tsm[False],
-             "split_planes_ms": split_ms,
+             "gen_ms": gen_ms, "panel_hbm_bytes": _panel_bytes(p),
              "note": "fmcore.step.ShardedStep at world 1 (HIP graph replay, timed like the headline): the "
                      "N=1 point of the c5 workload; ms_ts_gathered_100k = rank 4's share of the time-series "
                      "stage on the 100,000-month series an 8-rank all-gather assembles (its problem block's "
@@ -489,6 +487,15 @@ def _stream_copy_gbs(dev, nbytes=1 << 30, reps=10):
     del a, b
     torch.cuda.empty_cache()
     return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
+def _panel_bytes(panel):
+    """HBM bytes the panel holds (values in their layout, me, NYSE flags, month offsets)."""
+    n = 0
+    for t in (panel.cols, panel.planes, panel.me, panel.nyse, panel.seg_off):
+        if t is not None:
+            n += t.numel() * t.element_size()
+    return n
 
 
 def _lib_sha():
@@ -578,7 +585,7 @@ def cpu_baseline(panel, args, LW):
         threadpool_limits = None
     S = min(args.cpu_months, panel.nseg)
     n = S * args.firms
-    cols = {name: panel.cols[i, :n].cpu().numpy() for i, name in enumerate(panel.names)}
+    cols = {name: panel.column_host(i, n) for i, name in enumerate(panel.names)}
     me = panel.me[:n].cpu().numpy()
     nyse = panel.nyse[:n].cpu().numpy().astype(bool)
     seg = panel.seg_off_h[: S + 1]
@@ -606,7 +613,7 @@ def cpu_baseline(panel, args, LW):
             avail = os.cpu_count() or 1
         procs = max(1, min(args.cpu_procs, avail, 16))
         n_all = panel.nrows
-        cols_all = {name: panel.cols[i].cpu().numpy() for i, name in enumerate(panel.names)}
+        cols_all = {name: panel.column_host(i) for i, name in enumerate(panel.names)}
         sec, _ = MP.run(cols_all, panel.seg_off_h, panel.me.cpu().numpy(),
                         panel.nyse.cpu().numpy().astype(bool), models, procs)
         out["month_parallel"] = {"value": n_all / sec, "unit": "firm-month rows/s", "cores": procs,
@@ -632,7 +639,7 @@ def check_against_oracle(panel, gres, summ, args, LW):
     from oracle import fm_oracle as O
     S = 3
     n = S * args.firms
-    cols = {name: panel.cols[i, :n].cpu().numpy() for i, name in enumerate(panel.names)}
+    cols = {name: panel.column_host(i, n) for i, name in enumerate(panel.names)}
     models = {k: ("retx", v, (0, 1, 2)) for k, v in LW.table2_models().items()}
     ref = O.pipeline_arrays(cols, panel.seg_off_h[: S + 1], panel.me[:n].cpu().numpy(),
                             panel.nyse[:n].cpu().numpy().astype(bool), models, None)

@@ -30,6 +30,24 @@ int check_launch(const char* what);
 constexpr uint64_t SENT = ~0ull;   // key of NaN / absent values: sorts after +inf
 constexpr int WAVE = 64;
 
+// Panel values as FP64 columns or as the split panel's two 32-bit planes (high words, low
+// words; fm_gen_panel_planes / fm_split_planes): element i (= c * stride + r) either way.
+// The hot kernels read the planes with their own loads; this view serves the paths that
+// read individual values (pick gathers, fix-ups, refits).
+struct PCols {
+    const double* f = nullptr;
+    const uint32_t* h = nullptr;
+    const uint32_t* l = nullptr;
+    __device__ __forceinline__ double operator[](int64_t i) const {
+        if (f != nullptr) return f[i];
+        return __longlong_as_double((long long)(((uint64_t)h[i] << 32) | l[i]));
+    }
+    __device__ __forceinline__ PCols off(int64_t o) const {
+        return f != nullptr ? PCols{f + o, nullptr, nullptr} : PCols{nullptr, h + o, l + o};
+    }
+    __host__ __device__ __forceinline__ bool valid() const { return f != nullptr || (h != nullptr && l != nullptr); }
+};
+
 // Phase probe (timing builds only, tools/build_variant.sh probe "-DFM_PROBE=1" ...;
 // tools/tail_probe.py): thread 0 of a workgroup writes s_memrealtime (100 MHz) at numbered
 // points of a kernel into that translation unit's own bounded buffer (FM_PROBE_BUFFER), read

@@ -119,7 +119,9 @@ __global__ __launch_bounds__(ET) void gen_kernel(uint64_t seed, int64_t month0, 
                                                  uint64_t nyse_thr, uint64_t dy_thr,
                                                  double* __restrict__ cols, int64_t stride,
                                                  double* __restrict__ me,
-                                                 uint8_t* __restrict__ nyse) {
+                                                 uint8_t* __restrict__ nyse,
+                                                 uint32_t* __restrict__ hip_, uint32_t* __restrict__ lop,
+                                                 int64_t pstride) {
     const int64_t cell = (int64_t)blockIdx.x * ET + threadIdx.x;
     const int64_t ncell = (int64_t)nmonths * nfirms;
     if (cell >= ncell) return;
@@ -142,7 +144,12 @@ __global__ __launch_bounds__(ET) void gen_kernel(uint64_t seed, int64_t month0, 
     for (int k = 0; k < 15; ++k) {
         double v = x[k];
         if (nan_thr != 0 && cell_hash(seed, m, f, 32 + k) < nan_thr) v = NAN;
-        cols[(int64_t)k * stride + cell] = v;
+        if (cols != nullptr) cols[(int64_t)k * stride + cell] = v;
+        if (hip_ != nullptr) {   // the split layout, written here instead of by a later pass
+            const uint64_t u = (uint64_t)__double_as_longlong(v);
+            hip_[(int64_t)k * pstride + cell] = (uint32_t)(u >> 32);
+            lop[(int64_t)k * pstride + cell] = (uint32_t)u;
+        }
     }
     double mev = 10.0 / hash_u(cell_hash(seed, m, f, 64));
     if (me_nan_thr != 0 && cell_hash(seed, m, f, 65) < me_nan_thr) mev = NAN;
@@ -271,6 +278,27 @@ static uint64_t rate_thr(double r) {
     return (uint64_t)(r * 18446744073709551616.0);
 }
 
+extern "C" int fm_gen_panel_planes(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
+                                   double nan_rate, double nyse_rate, double* cols, int64_t col_stride,
+                                   uint32_t* hi, uint32_t* lo, int64_t plane_stride, double* me, uint8_t* nyse,
+                                   void* stream) {
+    using namespace fm;
+    FM_REQUIRE((cols || hi) && me && nyse && (hi == nullptr) == (lo == nullptr), "fm_gen_panel: null pointer");
+    FM_REQUIRE(nmonths >= 0 && nfirms > 0, "fm_gen_panel: bad sizes");
+    FM_REQUIRE(nan_rate >= 0.0 && nan_rate < 1.0 && nyse_rate > 0.0 && nyse_rate < 1.0,
+               "fm_gen_panel: rates must be in [0,1)");
+    const int64_t ncell = (int64_t)nmonths * nfirms;
+    FM_REQUIRE(cols == nullptr || col_stride >= ncell, "fm_gen_panel: col_stride < nmonths*nfirms");
+    FM_REQUIRE(hi == nullptr || plane_stride >= ncell, "fm_gen_panel: plane_stride < nmonths*nfirms");
+    if (ncell == 0) return FM_OK;
+    const int64_t nblk = (ncell + ET - 1) / ET;
+    hipLaunchKernelGGL(gen_kernel, dim3((unsigned)nblk), dim3(ET), 0, (hipStream_t)stream, seed,
+                       month0, nmonths, nfirms, rate_thr(nan_rate), rate_thr(0.25 * nan_rate),
+                       rate_thr(nyse_rate), rate_thr(0.3), cols, col_stride, me, nyse, hi, lo, plane_stride);
+    FM_CHECK_LAUNCH("fm_gen_panel");
+    return FM_OK;
+}
+
 extern "C" int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
                             double nan_rate, double nyse_rate, double* cols, int64_t col_stride,
                             double* me, uint8_t* nyse, void* stream) {
@@ -285,7 +313,7 @@ extern "C" int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int3
     const int64_t nblk = (ncell + ET - 1) / ET;
     hipLaunchKernelGGL(gen_kernel, dim3((unsigned)nblk), dim3(ET), 0, (hipStream_t)stream, seed,
                        month0, nmonths, nfirms, rate_thr(nan_rate), rate_thr(0.25 * nan_rate),
-                       rate_thr(nyse_rate), rate_thr(0.3), cols, col_stride, me, nyse);
+                       rate_thr(nyse_rate), rate_thr(0.3), cols, col_stride, me, nyse, nullptr, nullptr, 0);
     FM_CHECK_LAUNCH("fm_gen_panel");
     return FM_OK;
 }
@@ -300,6 +328,33 @@ extern "C" int fm_split_planes(const double* cols, int64_t col_stride, int32_t n
     hipLaunchKernelGGL(split_planes_kernel, dim3(4096), dim3(ET), 0, (hipStream_t)stream, cols, col_stride, ncols,
                        nrows, hi, lo, plane_stride);
     FM_CHECK_LAUNCH("fm_split_planes");
+    return FM_OK;
+}
+
+namespace fm {
+namespace {
+__global__ __launch_bounds__(ET) void merge_planes_kernel(const uint32_t* __restrict__ hi, const uint32_t* __restrict__ lo,
+                                                          int64_t pstride, int ncols, int64_t nrows,
+                                                          double* __restrict__ cols, int64_t stride) {
+    const int64_t total = nrows * ncols;
+    for (int64_t i = (int64_t)blockIdx.x * ET + threadIdx.x; i < total; i += (int64_t)gridDim.x * ET) {
+        const int64_t c = i / nrows, r = i - c * nrows;
+        cols[c * stride + r] =
+            __longlong_as_double((long long)(((uint64_t)hi[c * pstride + r] << 32) | lo[c * pstride + r]));
+    }
+}
+}  // namespace
+}  // namespace fm
+
+extern "C" int fm_merge_planes(const uint32_t* hi, const uint32_t* lo, int64_t plane_stride, int32_t ncols,
+                               int64_t nrows, double* cols, int64_t col_stride, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(cols && hi && lo, "fm_merge_planes: null pointer");
+    FM_REQUIRE(ncols >= 0 && nrows >= 0 && col_stride >= nrows && plane_stride >= nrows, "fm_merge_planes: bad sizes");
+    if (ncols == 0 || nrows == 0) return FM_OK;
+    hipLaunchKernelGGL(merge_planes_kernel, dim3(4096), dim3(ET), 0, (hipStream_t)stream, hi, lo, plane_stride, ncols,
+                       nrows, cols, col_stride);
+    FM_CHECK_LAUNCH("fm_merge_planes");
     return FM_OK;
 }
 

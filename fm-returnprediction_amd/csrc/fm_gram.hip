@@ -79,7 +79,8 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             const int kind = tid >> 5, c = tid & 31;
             const double* src = kind == 0 ? a.lo : kind == 1 ? a.hi : kind == 2 ? a.shift : a.inv_scale;
             const bool on = tid < 128 && c < ncols && src != nullptr;
-            const double* pp = on ? src + (int64_t)c * nseg + seg : a.cols;
+            // a valid dummy address when off (the FP64 columns may be absent on a split panel)
+            const double* pp = on ? src + (int64_t)c * nseg + seg : (const double*)a.seg_off;
             const double v = *pp;
             const double dflt = kind < 2 ? NAN : (kind == 2 ? 0.0 : 1.0);
             pv = on ? v : dflt;
@@ -130,7 +131,7 @@ extern "C" int fm_gram(const fm_gram_args* args, void* stream) {
     using namespace fm;
     FM_REQUIRE(args != nullptr, "fm_gram: null args");
     const fm_gram_args& a = *args;
-    FM_REQUIRE(a.cols && a.seg_off && a.chunk_seg && a.chunk_row && a.partial && a.flags &&
+    FM_REQUIRE((a.cols || a.hi_plane) && a.seg_off && a.chunk_seg && a.chunk_row && a.partial && a.flags &&
                    a.model_mask && a.model_ymask && a.pattern_id,
                "fm_gram: null pointer");
     FM_REQUIRE(a.ncols >= 1 && a.ncols <= FM_MAX_COLS, "fm_gram: ncols must be 1..%d", FM_MAX_COLS);

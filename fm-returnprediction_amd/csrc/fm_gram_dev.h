@@ -177,7 +177,7 @@ struct GramWave {
                 asm("" : "+s"(cb));
             }
         }
-        const uint8_t* lvbase = a.level ? a.level : (const uint8_t*)a.cols;
+        const uint8_t* lvbase = a.level ? a.level : (const uint8_t*)a.seg_off;   // any valid address
         // raw byte; masked where it is used (masking here would wait for the load)
         lv = *((gptr)(a.level ? lvbase + tb : lvbase) + (a.level ? lo : 0u));
     }

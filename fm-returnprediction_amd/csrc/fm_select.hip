@@ -53,7 +53,7 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
 __device__ __forceinline__ void stream_unit(const SelArgs& a, int s, int c, SelSmem& sm) {
     const int64_t r0 = a.seg_off[s];
     const int64_t L = a.seg_off[s + 1] - r0;
-    const double* src = a.cols + (int64_t)c * a.col_stride + r0;
+    const PCols src = sel_col(a, c, r0);
     const uint8_t* msk = a.mask ? a.mask + r0 : nullptr;
     // every pass streams the unit with SB loads per thread in flight (clamped, unconditional:
     // a load per loop iteration would wait out one memory round trip per value)
@@ -179,7 +179,7 @@ __device__ __forceinline__ void zero_sign_unit(const SelArgs& a, int s, int c, A
     if (!zl && !zh) return;
     const int64_t r0 = a.seg_off[s];
     const int L = (int)(a.seg_off[s + 1] - r0);
-    const double* src = a.cols + (int64_t)c * a.col_stride + r0;
+    const PCols src = sel_col(a, c, r0);
     const uint8_t* msk = a.mask ? a.mask + r0 : nullptr;
     // the values np.percentile sees: the unit's non-NaN (row-mask selected) rows, frame order
     auto fill = [&](bool& both) -> int {
@@ -795,7 +795,7 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
     const int64_t o = (int64_t)c * a.nseg + s;
     const int64_t r0 = a.seg_off[s];
     const int L = (int)(a.seg_off[s + 1] - r0);
-    const double* col = a.cols + (int64_t)c * a.col_stride + r0;
+    const PCols col = sel_col(a, c, r0);
     // rows past the month end (read as 0 by the range check) -> HK_NONE; straight-line (a
     // scalar branch per slot split the block and pushed keys into scratch)
     const int lim = L - tid;
@@ -1256,7 +1256,7 @@ __global__ __launch_bounds__(2 * WAVE) void select_pair_kernel(SelArgs a) {
     // finite min / max of this wave's half of unit u, re-read from memory: only the rare
     // pivot fallback (no finite cut midpoint) needs it, and by then xv holds the next unit
     auto finite_range = [&](int s, int c, double& m1, double& m2) {
-        const double* base = a.cols + (int64_t)c * a.col_stride + a.seg_off[s];
+        const PCols base = sel_col(a, c, a.seg_off[s]);
         const int Lu = (int)(a.seg_off[s + 1] - a.seg_off[s]);
         m1 = NAN;
         m2 = NAN;
@@ -1504,7 +1504,7 @@ struct PairHkSmem {
 // about 230 here.)  false: cannot decide (never expected).
 template <int R>
 __device__ __forceinline__ bool pick_hk(uint64_t* L1, int c1, const uint64_t* L2, int c2, int ra, int rb, int tail,
-                                        const double* col, double& va, double& vb) {
+                                        const PCols col, double& va, double& vb) {
     const int lane = lane_id();
     const int c = c1 + c2;
     uint32_t key[R], row[R], sk[R];
@@ -1614,7 +1614,7 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
         return L;
     };
     auto finite_range = [&](int s, int c, double& m1, double& m2) {
-        const double* base = a.cols + (int64_t)c * a.col_stride + a.seg_off[s];
+        const PCols base = sel_col(a, c, a.seg_off[s]);
         const int Lu = (int)(a.seg_off[s + 1] - a.seg_off[s]);
         m1 = NAN;
         m2 = NAN;
@@ -1766,7 +1766,7 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
             const int cc = c0 + c1;
             bool good = c0 <= WCAP && c1 <= WCAP && cc <= 4 * WAVE;
             if (good) {
-                const double* col = a.cols + (int64_t)c_cur * a.col_stride + a.seg_off[s_cur];
+                const PCols col = sel_col(a, c_cur, a.seg_off[s_cur]);
                 const int ra = t == 0 ? i0 : n - 1 - j1, rb = t == 0 ? j0 : n - 1 - i1;
                 double va = NAN, vb = NAN;
                 if (cc <= WAVE) good = pick_hk<1>(sm.cand[0][t], c0, sm.cand[1][t], c1, ra, rb, t, col, va, vb);
@@ -2116,7 +2116,7 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
     const int32_t ncols = x.ncols, nseg = x.nseg, max_seg_len = x.max_seg_len;
     const uint8_t* row_mask = x.row_mask;
     const int32_t* nvalid = x.nvalid;
-    FM_REQUIRE(cols && seg_off && x.lo && x.hi, "fm_select_cuts: null pointer");
+    FM_REQUIRE((cols || (x.hi_plane && x.lo_plane)) && seg_off && x.lo && x.hi, "fm_select_cuts: null pointer");
     FM_REQUIRE(ncols > 0 && ncols <= 65535 && nseg >= 0, "fm_select_cuts: bad sizes");
     FM_REQUIRE(x.lerp_mode == 0 || x.lerp_mode == 1, "fm_select_cuts: lerp_mode must be 0 or 1");
     FM_REQUIRE(x.q_lo >= 0.0 && x.q_lo <= 1.0 && x.q_hi >= 0.0 && x.q_hi <= 1.0,
@@ -2130,7 +2130,12 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
     a.ctl = (SelCtl*)x.ws;
     a.hp = x.hi_plane;
     a.pstride = x.plane_stride;
+    a.lp = x.lo_plane;
     FM_REQUIRE(a.hp == nullptr || a.pstride > 0, "fm_select: hi_plane needs plane_stride > 0");
+    FM_REQUIRE(a.lp == nullptr || a.hp != nullptr, "fm_select: lo_plane needs hi_plane");
+    // a split panel without FP64 columns: only the plane-reading paths (the two-wave and
+    // long-month high-key kernels, the workgroup / streaming fix-ups) can serve it
+    const bool no_f64 = cols == nullptr;
     hipStream_t st = (hipStream_t)stream;
     const int vpt = (max_seg_len + ST - 1) / ST;
     const bool long_path = vpt > FM_SELECT_STREAM_VPT && max_seg_len <= LONG_VPT * LT && x.mean == nullptr &&
@@ -2151,6 +2156,8 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
     if (long_path) {
         // past the 256-thread paths' register budget: the 512-thread register-resident
         // kernel (one read per unit); the streaming kernel redoes the units it marked
+        FM_REQUIRE(!no_f64 || (a.hp != nullptr && !long_is_mid(a, max_seg_len) && !FM_AB_LONG_F64 && FM_AB_LONG == 0),
+                   "fm_select: this long-month path (row mask / middle ranks) needs FP64 columns");
         SelArgs al = a;
         if (ride) set_universe(al, u);
         const int rc = launch_select_long(al, max_seg_len, st);
@@ -2182,6 +2189,8 @@ int select_impl(const fm_select_args* args, const fm_universe_args* u, void* str
     const bool wave = row_mask == nullptr && nvalid != nullptr && vpl <= 96;
 #endif
     (void)vpl;
+    FM_REQUIRE(!no_f64 || (wave && x.mean == nullptr && a.hp != nullptr) || !wave,
+               "fm_select: moments on a split panel need FP64 columns");
     if (wave && x.mean == nullptr && vpl <= 96 && !getenv_flag_one_wave()) {
         // two waves per unit (the common Table-2 case: no moments)
         const int rc = launch_select_pair_vph(a, max_seg_len, st);

@@ -85,7 +85,17 @@ struct SelArgs {
     // and long-month kernels then read 4 bytes per value
     const uint32_t* hp = nullptr;
     int64_t pstride = 0;
+    // fm_select_args.lo_plane: with hp, the low words; cols may then be NULL (a split panel
+    // without FP64 columns): the gathers and fix-up paths read values through sel_col
+    const uint32_t* lp = nullptr;
 };
+
+// Column c of the panel from row r0 on, as FP64 values or from the two planes
+__device__ __forceinline__ PCols sel_col(const SelArgs& a, int c, int64_t r0) {
+    if (a.cols != nullptr) return PCols{a.cols + (int64_t)c * a.col_stride + r0, nullptr, nullptr};
+    const int64_t o = (int64_t)c * a.pstride + r0;
+    return PCols{nullptr, a.hp + o, a.lp + o};
+}
 
 // One lane: unit u goes on the fix-up kernel's worklist (and is marked, nvalid = -1, when the
 // kernel could not finish it).  A call pushes each of its nseg * ncols units at most once, so
@@ -760,7 +770,17 @@ __device__ __forceinline__ void select_unit_wg(const SelArgs& a, int s, int c, S
     uint32_t lb = (uint32_t)threadIdx.x * 8u;
     asm volatile("" : "+v"(lb));
     double xv[VPT];
-    if (a.mask == nullptr) {   // block-uniform
+    if (a.cols == nullptr) {   // block-uniform: a split panel without FP64 columns (fix-up path)
+        const PCols pc = sel_col(a, c, r0);
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            const uint32_t off = lb + (uint32_t)(v * NT * 8);
+            const uint32_t oc = off < lastb ? off : lastb;
+            const double x = pc[oc >> 3];
+            const bool m = a.mask == nullptr || a.mask[r0 + (oc >> 3)] != 0;
+            xv[v] = (off <= lastb && L > 0 && m) ? x : NAN;
+        }
+    } else if (a.mask == nullptr) {   // block-uniform
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
             const uint32_t off = lb + (uint32_t)(v * NT * 8);

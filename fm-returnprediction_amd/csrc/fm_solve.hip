@@ -393,7 +393,7 @@ template <int NC, int NT>
 union FixSmem;
 inline __device__ bool fix_wanted(uint32_t st, int check_const);
 template <int NC, int NT>
-__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, const double* cols, int64_t stride,
+__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, PCols cols, int64_t stride,
                         const int64_t* seg_off, int nseg, const double* lo, const double* hi,
                         const double* shift, const double* inv_scale, const double* add_back,
                         const uint8_t* level, int nprob, const int32_t* prob_level, const int32_t* prob_z,
@@ -695,13 +695,14 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     FM_PROBE_AT(solve, 3);
     // the statsmodels fix-ups of this month's flagged problems (fm_solve_fixup's work, rare),
     // by this workgroup: its own rec / moments / status writes are visible after the barrier
-    if (a.fix_cols != nullptr) {   // block-uniform
+    const PCols fcols{a.fix_cols, a.fix_hi_plane, a.fix_lo_plane};
+    if (fcols.valid()) {   // block-uniform
         __syncthreads();
         const int ckc = a.fix_check_const;
         for (int q = 0; q < a.nprob; ++q) {
             const uint32_t st = t_st[q];
             if (!fix_wanted(st, ckc)) continue;   // block-uniform
-            fix_one<G16, S16T>(s, q, st, *reinterpret_cast<FixSmem<G16, S16T>*>(&wsc[0][0]), a.fix_cols,
+            fix_one<G16, S16T>(s, q, st, *reinterpret_cast<FixSmem<G16, S16T>*>(&wsc[0][0]), fcols,
                                a.fix_stride, a.fix_seg_off, a.nseg, a.fix_lo, a.fix_hi, a.fix_shift,
                                a.fix_inv_scale, a.add_back, a.fix_level, a.nprob, a.prob_level, a.prob_z,
                                a.prob_nz, a.moments, a.mom_stride, a.pmax, a.rec, a.status, ckc);
@@ -712,7 +713,7 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
 // Exact nonzero-constant test for problems flagged CONST_SUSPECT (statsmodels
 // add_constant(has_constant='skip'): np.ptp(x)==0 & all(x != 0), src/regressions.py:50).
 template <int NT = VT>
-__device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, const double* cols, int64_t stride,
+__device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, PCols cols, int64_t stride,
                                            const int64_t* seg_off, int nseg, const double* lo,
                                            const double* hi, const uint8_t* level, int nprob,
                                            const int32_t* prob_level, const int32_t* prob_z,
@@ -754,7 +755,7 @@ __device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, const do
     if (threadIdx.x == 0 && any_const) status[(int64_t)s * nprob + p] |= FM_ST_CONST_COL;
 }
 
-__global__ __launch_bounds__(VT) void const_kernel(const double* cols, int64_t stride, int ncols,
+__global__ __launch_bounds__(VT) void const_kernel(PCols cols, int64_t stride, int ncols,
                                                    const int64_t* seg_off, int nseg,
                                                    const double* lo, const double* hi,
                                                    const uint8_t* level, int nprob,
@@ -793,7 +794,7 @@ struct InfySmem {
 };
 
 template <int NT = VT, int NC = 32>
-__device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, const double* cols, int64_t stride,
+__device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, PCols cols, int64_t stride,
                                           const int64_t* seg_off, int nseg, const double* lo,
                                           const double* hi, const double* shift,
                                           const double* inv_scale, const double* add_back,
@@ -1044,7 +1045,7 @@ __device__ __forceinline__ void hh_absorb(double (&a)[NC], double (*R)[NC + 1], 
 }
 
 template <int NC, int NT = VT>
-__device__ void refit_pair(int s, int p, RefitSmem<NC, NT / WAVE>& sm, const double* cols, int64_t stride,
+__device__ void refit_pair(int s, int p, RefitSmem<NC, NT / WAVE>& sm, PCols cols, int64_t stride,
                            const int64_t* seg_off, int nseg, const double* lo, const double* hi,
                            const double* shift, const double* inv_scale, const double* add_back,
                            const uint8_t* level, int nprob, const int32_t* prob_level,
@@ -1203,7 +1204,7 @@ inline __device__ bool fix_wanted(uint32_t st, int check_const) {
 // The fix-ups of one flagged (month, problem) whose solve status is `st`, by the whole
 // NT-thread workgroup (block-uniform; ends with the workgroup synchronized)
 template <int NC, int NT>
-__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, const double* cols,
+__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, PCols cols,
                                         int64_t stride, const int64_t* seg_off, int nseg, const double* lo,
                                         const double* hi, const double* shift, const double* inv_scale,
                                         const double* add_back, const uint8_t* level, int nprob,
@@ -1229,7 +1230,7 @@ __device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, N
 }
 
 template <int NC>
-__global__ __launch_bounds__(VT) void fixup_kernel(const double* cols, int64_t stride,
+__global__ __launch_bounds__(VT) void fixup_kernel(PCols cols, int64_t stride,
                                                    const int64_t* seg_off, int nseg, const double* lo,
                                                    const double* hi, const double* shift,
                                                    const double* inv_scale, const double* add_back,
@@ -1298,7 +1299,9 @@ extern "C" int fm_solve(const fm_solve_args* args, void* stream) {
     FM_REQUIRE(a.add_back == nullptr || (a.ab_ncols >= 1 && a.ab_ncols <= FM_MAX_COLS),
                "fm_solve: add_back needs ab_ncols in 1..%d", FM_MAX_COLS);
     FM_REQUIRE(a.zw == 32 || a.nprob <= S16_MAXP, "fm_solve: at most %d problems per group", S16_MAXP);
-    FM_REQUIRE(a.fix_cols == nullptr || (a.zw == 16 && a.fix_seg_off && a.moments && a.pmax + 1 <= 16 &&
+    FM_REQUIRE((a.fix_hi_plane == nullptr) == (a.fix_lo_plane == nullptr),
+               "fm_solve: fix_hi_plane and fix_lo_plane go together");
+    FM_REQUIRE((a.fix_cols == nullptr && a.fix_hi_plane == nullptr) || (a.zw == 16 && a.fix_seg_off && a.moments && a.pmax + 1 <= 16 &&
                                          (a.fix_lo == nullptr) == (a.fix_hi == nullptr) &&
                                          (a.fix_inv_scale == nullptr || a.fix_shift != nullptr)),
                "fm_solve: inline fix-ups need zw 16, fix_seg_off, moments, pmax <= 15, lo with hi, "
@@ -1334,7 +1337,7 @@ extern "C" int fm_const_check(const double* cols, int64_t col_stride, int32_t nc
     const int64_t work = npairs < 0 ? (int64_t)nseg * nprob : npairs;
     if (work == 0) return FM_OK;
     const int grid = (int)(npairs < 0 ? (work < SCAN_GRID ? work : SCAN_GRID) : work);
-    hipLaunchKernelGGL(const_kernel, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols,
+    hipLaunchKernelGGL(const_kernel, dim3(grid), dim3(VT), 0, (hipStream_t)stream, PCols{cols, nullptr, nullptr},
                        col_stride, ncols, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
                        prob_nz, pairs, npairs, status);
     FM_CHECK_LAUNCH("fm_const_check");
@@ -1359,12 +1362,12 @@ extern "C" int fm_solve_fixup(const double* cols, int64_t col_stride, const int6
     const int64_t ranges = (work + VT - 1) / VT;   // VT pairs per workgroup pass
     const int grid = (int)(ranges < SCAN_GRID ? ranges : SCAN_GRID);
     if (pmax + 1 <= 16)
-        hipLaunchKernelGGL(fixup_kernel<16>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
-                           seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
+        hipLaunchKernelGGL(fixup_kernel<16>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, PCols{cols, nullptr, nullptr},
+                           col_stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
                            prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status, check_const);
     else
-        hipLaunchKernelGGL(fixup_kernel<32>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, cols, col_stride,
-                           seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
+        hipLaunchKernelGGL(fixup_kernel<32>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, PCols{cols, nullptr, nullptr},
+                           col_stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
                            prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status, check_const);
     FM_CHECK_LAUNCH("fm_solve_fixup");
     return FM_OK;

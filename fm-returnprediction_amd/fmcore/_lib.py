@@ -53,7 +53,7 @@ class SelectArgs(C.Structure):
         ("max_seg_len", _i32), ("row_mask", _p), ("q_lo", _f64), ("q_hi", _f64),
         ("min_count", _i32), ("lerp_mode", _i32), ("lo", _p), ("hi", _p), ("nvalid", _p),
         ("mean", _p), ("sd", _p), ("center", _p), ("level", _p), ("ws", _p),
-        ("hi_plane", _p), ("plane_stride", _i64),
+        ("hi_plane", _p), ("plane_stride", _i64), ("lo_plane", _p),
     ]
 
 
@@ -89,6 +89,8 @@ class SolveArgs(C.Structure):
         ("fix_cols", _p), ("fix_stride", _i64), ("fix_seg_off", _p), ("fix_lo", _p), ("fix_hi", _p),
         ("fix_shift", _p), ("fix_inv_scale", _p), ("fix_level", _p), ("fix_check_const", _i32),
         ("fix_pad", _i32),
+        # a planes-only panel's fix-up rows (fix_cols None; stride = fix_stride)
+        ("fix_hi_plane", _p), ("fix_lo_plane", _p),
     ]
 
 
@@ -143,6 +145,8 @@ _SIGS = {
     "fm_rolling_std": (_i32, [_p, _p, _i64, _i32, _i32, _f64, _p, _p]),
     "fm_rolling_beta": (_i32, [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p]),
     "fm_gen_panel": (_i32, [C.c_uint64, _i64, _i32, _i32, _f64, _f64, _p, _i64, _p, _p, _p]),
+    "fm_gen_panel_planes": (_i32, [C.c_uint64, _i64, _i32, _i32, _f64, _f64, _p, _i64, _p, _p, _i64, _p, _p, _p]),
+    "fm_merge_planes": (_i32, [_p, _p, _i64, _i32, _i64, _p, _i64, _p]),
     "fm_stream_probe": (_i32, [_p, _i64, _p, _p]),
 }
 

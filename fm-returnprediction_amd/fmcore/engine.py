@@ -4,9 +4,13 @@ torch (ROCm) only provides device buffers and the stream; every computation on t
 path is a libfm_hip kernel.  There is no CPU fallback: without a HIP device the
 functions raise.
 
-Layout in HBM (``DevicePanel``): one FP64 SoA block ``cols[C, n]`` with rows sorted by
-(month, input order) — month segments are CSR ``seg_off[T+1]`` — plus optional ``me``
-(FP64) and ``nyse`` (uint8) rows and a uint8 universe ``level`` per row.
+Layout in HBM (``DevicePanel``): the panel's C columns with rows sorted by (month, input
+order) -- month segments are CSR ``seg_off[T+1]`` -- as an FP64 SoA block ``cols[C, n]``
+and/or the split layout ``planes[2, C, n]`` (uint32 high / low words: the selects read the
+high plane, the Gram both), plus optional ``me`` (FP64) and ``nyse`` (uint8) rows and a
+uint8 universe ``level`` per row.  A panel built with ``layout="planes"`` holds no FP64
+columns at all (half the HBM): the whole Table-2 pass reads the planes, and consumers of
+FP64 columns (clip, forecasts, moments) get them from ``values()``.
 """
 from __future__ import annotations
 
@@ -114,7 +118,7 @@ def _stream():
 # ------------------------------------------------------------------------------------------
 @dataclass
 class DevicePanel:
-    cols: torch.Tensor                 # [C, n] float64, contiguous
+    cols: Optional[torch.Tensor]       # [C, n] float64, contiguous (None: a planes-only panel)
     names: List[str]
     seg_off: torch.Tensor              # [T+1] int64 (device)
     seg_off_h: np.ndarray              # [T+1] int64 (host)
@@ -124,9 +128,47 @@ class DevicePanel:
     order: Optional[np.ndarray] = None   # sorted row -> original positional row
     chunk_rows: Optional[int] = None     # Gram chunking override (sharded runs: global policy)
     chunk_split: Optional[bool] = None   # split-month Gram plan (make_chunks_split) override
-    planes: Optional[torch.Tensor] = None   # [2, C, n] uint32: cols' high / low words (split_planes)
+    planes: Optional[torch.Tensor] = None   # [2, C, n] int32: the values' high / low words
     chunk_policy: Optional[tuple] = None    # Gram plan of the GLOBAL panel (chunk_policy()), sharded runs
     row_origin: int = 0                     # global row of this panel's row 0 (balanced plans)
+    planes_version: int = -1                # cols._version when the planes were made from cols
+
+    @property
+    def device(self):
+        return (self.cols if self.cols is not None else self.planes).device
+
+    def values(self):
+        """The FP64 columns [C, n]: ``cols``, or for a planes-only panel a device merge of the
+        planes (fm_merge_planes), made once and kept.  Off the Table-2 hot path (clip,
+        forecasts, moments, the standardize variant)."""
+        if self.cols is not None:
+            return self.cols
+        m = self.__dict__.get("_merged")
+        if m is None:
+            C, n = self.planes.shape[1], self.planes.shape[2]
+            m = torch.empty((C, n), dtype=torch.float64, device=self.planes.device)
+            _kcall("fm_merge_planes", "fm_merge_planes", self.planes[0].data_ptr(), self.planes[1].data_ptr(),
+                   self.planes.stride(1), C, n, m.data_ptr(), m.stride(0), _stream())
+            self.__dict__["_merged"] = m
+        return m
+
+    def column_host(self, i, n=None):
+        """Column i (its first n rows) as a host float64 array, from the planes without an
+        FP64 device copy when the panel has none."""
+        n = self.nrows if n is None else n
+        if self.cols is not None:
+            return self.cols[i, :n].cpu().numpy()
+        hi = self.planes[0, i, :n].cpu().numpy().astype(np.uint32).astype(np.uint64)
+        lo = self.planes[1, i, :n].cpu().numpy().astype(np.uint32).astype(np.uint64)
+        return ((hi << np.uint64(32)) | lo).view(np.float64)
+
+    def check_planes(self):
+        """The planes must still be the FP64 columns' words: an in-place write to ``cols``
+        after the planes were made (torch bumps the tensor's version counter) is refused."""
+        if self.planes is not None and self.cols is not None and self.planes_version >= 0 and \
+                self.cols._version != self.planes_version:
+            raise RuntimeError("panel.cols was modified in place after its planes were made: call "
+                               "split_planes(panel) again (or build a new panel)")
 
     @property
     def nrows(self):
@@ -138,11 +180,11 @@ class DevicePanel:
 
     @property
     def ncols(self):
-        return self.cols.shape[0]
+        return self.cols.shape[0] if self.cols is not None else self.planes.shape[1]
 
     @property
     def stride(self):
-        return self.cols.stride(0)
+        return self.values().stride(0)
 
     @property
     def max_seg_len(self):
@@ -169,9 +211,29 @@ def month_segments(labels):
     return codes, uniq, order, seg_off
 
 
+def gather_layout(raw, perm, layout="f64"):
+    """The device gather of an ingest: FP64 columns ``raw`` [C, n_in] (input row order) ->
+    month-major rows in the panel's layout, (cols, planes): "f64" the FP64 columns, "planes"
+    the high / low 32-bit words gathered straight from the raw words (no FP64 panel copy),
+    "both"."""
+    if layout not in PANEL_LAYOUTS:
+        raise ValueError(f"layout must be one of {PANEL_LAYOUTS}")
+    cols = planes = None
+    if layout != "planes":
+        cols = raw.index_select(1, perm).contiguous()
+    if layout != "f64":
+        C = raw.shape[0]
+        words = raw.contiguous().view(torch.int32).view(C, -1, 2)   # little-endian: [..., 1] = high word
+        planes = torch.empty((2, C, max(perm.numel(), 1)), dtype=torch.int32, device=raw.device)
+        planes[0, :, :perm.numel()] = words[:, :, 1].index_select(1, perm)
+        planes[1, :, :perm.numel()] = words[:, :, 0].index_select(1, perm)
+    return cols, planes
+
+
 def panel_from_arrays(arrays: Sequence[np.ndarray], names, labels, me=None, nyse=None,
-                      device=None):
-    """Upload host columns (original row order) and permute them month-major on device."""
+                      device=None, layout="f64"):
+    """Upload host columns (original row order) and permute them month-major on device, into
+    the panel's ``layout`` ("f64", "planes": the split layout only, "both")."""
     device = device or require_device()
     _, uniq, order, seg_off = month_segments(labels)
     n_in = len(labels)
@@ -180,14 +242,17 @@ def panel_from_arrays(arrays: Sequence[np.ndarray], names, labels, me=None, nyse
         host[i] = np.asarray(a, dtype=np.float64)
     raw = torch.from_numpy(host).to(device, non_blocking=False)
     perm = torch.from_numpy(order.astype(np.int64)).to(device)
-    cols = raw.index_select(1, perm).contiguous()
+    cols, planes = gather_layout(raw, perm, layout)
     me_t = nyse_t = None
     if me is not None:
         me_t = torch.from_numpy(np.asarray(me, dtype=np.float64)).to(device).index_select(0, perm)
     if nyse is not None:
         nyse_t = torch.from_numpy(np.asarray(nyse, dtype=np.uint8)).to(device).index_select(0, perm)
-    return DevicePanel(cols=cols, names=list(names), seg_off=torch.from_numpy(seg_off).to(device),
-                       seg_off_h=seg_off, months=uniq, me=me_t, nyse=nyse_t, order=order)
+    p = DevicePanel(cols=cols, names=list(names), seg_off=torch.from_numpy(seg_off).to(device),
+                    seg_off_h=seg_off, months=uniq, me=me_t, nyse=nyse_t, order=order, planes=planes)
+    if cols is not None and planes is not None:
+        p.planes_version = cols._version
+    return p
 
 
 def split_planes(panel: DevicePanel):
@@ -200,31 +265,78 @@ def split_planes(panel: DevicePanel):
     _kcall("fm_split_planes", "fm_split_planes", panel.cols.data_ptr(), panel.stride, C, n, planes[0].data_ptr(),
            planes[1].data_ptr(), planes.stride(1), _stream())
     panel.planes = planes
+    panel.planes_version = panel.cols._version
     return panel
 
 
-def _planes_for(panel: DevicePanel, src):
-    """(hi, lo, stride) when ``src`` is the panel's own columns and they are split."""
-    pl = panel.planes
-    if pl is None or src.data_ptr() != panel.cols.data_ptr() or src.shape[0] != panel.ncols:
-        return None, None, 0
-    return pl[0].data_ptr(), pl[1].data_ptr(), pl.stride(1)
+@dataclass
+class _Src:
+    """What a panel kernel reads: FP64 columns (``f64``) and/or the panel's planes."""
+    f64: Optional[torch.Tensor]
+    hp: Optional[int]
+    lp: Optional[int]
+    pstride: int
+    ncols: int
+    device: object
+
+    @property
+    def ptr(self):
+        return None if self.f64 is None else self.f64.data_ptr()
+
+    @property
+    def stride(self):
+        return self.f64.stride(0) if self.f64 is not None else self.pstride
 
 
-def panel_synthetic(nmonths, nfirms, seed, month0=0, nan_rate=0.02, nyse_rate=0.4, device=None):
+def _source(panel: DevicePanel, cols=None):
+    """``cols`` given: those FP64 columns only.  Else the panel's own values: its FP64
+    columns, its planes, or both (a planes-only panel: no FP64 pointer at all)."""
+    if cols is not None:
+        cols = cols.view(1, -1) if cols.dim() == 1 else cols
+        return _Src(cols, None, None, 0, cols.shape[0], cols.device)
+    panel.check_planes()
+    hp = lp = None
+    ps = 0
+    if panel.planes is not None:
+        hp, lp, ps = panel.planes[0].data_ptr(), panel.planes[1].data_ptr(), panel.planes.stride(1)
+    return _Src(panel.cols, hp, lp, ps, panel.ncols, panel.device)
+
+
+PANEL_LAYOUTS = ("f64", "planes", "both")
+
+
+def panel_synthetic(nmonths, nfirms, seed, month0=0, nan_rate=0.02, nyse_rate=0.4, device=None, layout="f64"):
     """Generate a balanced synthetic panel directly in HBM (fm_gen_panel; identical to
-    fmcore.synth.synth_arrays with present_rate=1)."""
+    fmcore.synth.synth_arrays with present_rate=1).  ``layout``: "f64" the FP64 columns,
+    "planes" only the split layout (fm_gen_panel_planes writes the high / low words itself:
+    no FP64 columns, no layout pass), "both"."""
     from .synth import WINSOR_VARS
+    if layout not in PANEL_LAYOUTS:
+        raise ValueError(f"layout must be one of {PANEL_LAYOUTS}")
     device = device or require_device()
     n = nmonths * nfirms
-    cols = torch.empty((len(WINSOR_VARS), n), dtype=torch.float64, device=device)
+    C = len(WINSOR_VARS)
+    cols = planes = None
+    if layout != "planes":
+        cols = torch.empty((C, n), dtype=torch.float64, device=device)
+    if layout != "f64":
+        planes = torch.empty((2, C, max(n, 1)), dtype=torch.int32, device=device)
     me = torch.empty(n, dtype=torch.float64, device=device)
     nyse = torch.empty(n, dtype=torch.uint8, device=device)
-    _kcall("fm_gen_panel", "fm_gen_panel", seed, month0, nmonths, nfirms, nan_rate, nyse_rate, cols.data_ptr(),
-           cols.stride(0), me.data_ptr(), nyse.data_ptr(), _stream())
+    if planes is None:
+        _kcall("fm_gen_panel", "fm_gen_panel", seed, month0, nmonths, nfirms, nan_rate, nyse_rate, cols.data_ptr(),
+               cols.stride(0), me.data_ptr(), nyse.data_ptr(), _stream())
+    else:
+        _kcall("fm_gen_panel", "fm_gen_panel_planes", seed, month0, nmonths, nfirms, nan_rate, nyse_rate, _ptr(cols),
+               cols.stride(0) if cols is not None else 0, planes[0].data_ptr(), planes[1].data_ptr(),
+               planes.stride(1), me.data_ptr(), nyse.data_ptr(), _stream())
     seg_off = np.arange(nmonths + 1, dtype=np.int64) * nfirms
-    return DevicePanel(cols=cols, names=list(WINSOR_VARS), seg_off=torch.from_numpy(seg_off).to(device),
-                       seg_off_h=seg_off, months=np.arange(month0, month0 + nmonths), me=me, nyse=nyse)
+    p = DevicePanel(cols=cols, names=list(WINSOR_VARS), seg_off=torch.from_numpy(seg_off).to(device),
+                    seg_off_h=seg_off, months=np.arange(month0, month0 + nmonths), me=me, nyse=nyse,
+                    planes=planes)
+    if cols is not None and planes is not None:
+        p.planes_version = cols._version
+    return p
 
 
 # ------------------------------------------------------------------------------------------
@@ -272,10 +384,13 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
     launch for months of <= 5,120 rows, riding the long-month kernel's launch for
     6,145-20,480-row months without the histogram (MID) variant, its own launch first
     otherwise); returns (Cuts, (cut_a, cut_b, level)) then."""
-    src = panel.cols if cols is None else cols
-    if src.dim() == 1:
-        src = src.view(1, -1)
-    C, T = src.shape[0], panel.nseg
+    if cols is not None:
+        src = _source(panel, cols)
+    elif row_mask is not None or moments:   # the row-masked and moments paths read FP64 columns
+        src = _source(panel, panel.values())
+    else:
+        src = _source(panel)
+    C, T = src.ncols, panel.nseg
     dev = src.device
     lo = torch.empty((C, T), dtype=torch.float64, device=dev)
     hi = torch.empty_like(lo)
@@ -288,15 +403,16 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
         cen = torch.empty_like(lo)
     msl = max(panel.max_seg_len, 1)
     ws = select_ws(T, C, msl, dev)
-    hp, _, pst = _planes_for(panel, src) if row_mask is None else (None, None, 0)
-    sa = L.SelectArgs(cols=src.data_ptr(), col_stride=src.stride(0), ncols=C, seg_off=panel.seg_off.data_ptr(),
+    sa = L.SelectArgs(cols=src.ptr, col_stride=src.stride if src.f64 is not None else 0, ncols=C,
+                      seg_off=panel.seg_off.data_ptr(),
                       nseg=T, max_seg_len=msl, row_mask=_ptr(row_mask), q_lo=float(q_lo),
                       q_hi=float(q_hi), min_count=int(min_count), lerp_mode=int(mode), lo=lo.data_ptr(),
                       hi=hi.data_ptr(), nvalid=nv.data_ptr(), mean=_ptr(mean), sd=_ptr(sd), center=_ptr(cen),
-                      level=_ptr(level), ws=ws.data_ptr(), hi_plane=hp, plane_stride=pst)
+                      level=_ptr(level), ws=ws.data_ptr(), hi_plane=src.hp, plane_stride=src.pstride,
+                      lo_plane=src.lp)
     if universe is None:
         _kcall(tag, "fm_select", L.C.byref(sa), _stream())
-        _remember(tag, "fm_select", sa, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, level)
+        _remember(tag, "fm_select", sa, src, panel.planes, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, level)
         return Cuts(lo, hi, nv, mean, sd, cen)
     ca = torch.empty(T, dtype=torch.float64, device=dev)
     cb = torch.empty_like(ca)
@@ -306,21 +422,22 @@ def select_cuts(panel: DevicePanel, q_lo, q_hi, min_count, mode=LERP_NUMPY, cols
     _kcall(tag, "fm_select_universe", L.C.byref(sa), L.C.byref(ua), _stream())
     # re-issued by time_launch with both structs (keep[1] holds the argument tuple)
     LAST_LAUNCH[tag] = ("fm_select_universe", None,
-                        ((sa, ua, src, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, panel.me, panel.nyse,
+                        ((sa, ua, src, panel.planes, lo, hi, nv, mean, sd, cen, row_mask, panel.seg_off, panel.me, panel.nyse,
                           ca, cb, ulev), (L.C.byref(sa), L.C.byref(ua))))
     return Cuts(lo, hi, nv, mean, sd, cen), (ca, cb, ulev)
 
 
 def clip(panel: DevicePanel, cuts: Cuts, out=None):
-    out = torch.empty_like(panel.cols) if out is None else out
-    _kcall("fm_clip", "fm_clip", panel.cols.data_ptr(), out.data_ptr(), panel.stride, panel.ncols,
+    v = panel.values()
+    out = torch.empty_like(v) if out is None else out
+    _kcall("fm_clip", "fm_clip", v.data_ptr(), out.data_ptr(), v.stride(0), panel.ncols,
            panel.seg_off.data_ptr(), panel.nseg, panel.nrows, cuts.lo.data_ptr(), cuts.hi.data_ptr(),
            _stream())
     return out
 
 
 def standardize(panel: DevicePanel, mean, sd, src=None, out=None):
-    src = panel.cols if src is None else src
+    src = panel.values() if src is None else src
     out = torch.empty_like(src) if out is None else out
     _kcall("fm_standardize", "fm_standardize", src.data_ptr(), out.data_ptr(), src.stride(0), src.shape[0],
            panel.seg_off.data_ptr(), panel.nseg, panel.nrows, mean.data_ptr(), sd.data_ptr(),
@@ -337,7 +454,7 @@ def nyse_breakpoints(panel: DevicePanel, q_a=0.2, q_b=0.5, level=None):
 
 
 def universe_level(panel: DevicePanel, cut_a, cut_b):
-    level = torch.empty(panel.nrows, dtype=torch.uint8, device=panel.cols.device)
+    level = torch.empty(panel.nrows, dtype=torch.uint8, device=panel.device)
     _kcall("fm_universe_level", "fm_universe_level", panel.me.data_ptr(), panel.seg_off.data_ptr(), panel.nseg,
            panel.nrows, cut_a.data_ptr(), cut_b.data_ptr(), level.data_ptr(), _stream())
     return level
@@ -349,10 +466,10 @@ def universe(panel: DevicePanel, q_a=0.2, q_b=0.5):
     (fm_universe); months longer than its register budget take fm_select (row mask, the
     level bytes written by the same call).  Returns (cut_a [T], cut_b [T], level [rows] uint8)."""
     if panel.max_seg_len > UNIVERSE_MAX_ROWS:
-        level = torch.empty(panel.nrows, dtype=torch.uint8, device=panel.cols.device)
+        level = torch.empty(panel.nrows, dtype=torch.uint8, device=panel.device)
         a, b = nyse_breakpoints(panel, q_a, q_b, level=level)
         return a, b, level
-    dev = panel.cols.device
+    dev = panel.device
     a = torch.empty(panel.nseg, dtype=torch.float64, device=dev)
     b = torch.empty_like(a)
     level = torch.empty(panel.nrows, dtype=torch.uint8, device=dev)
@@ -370,7 +487,7 @@ SELECT_LONG_MIN, SELECT_LONG_MAX = 24 * 256, 40 * 512
 
 
 def pilot_shift(panel: DevicePanel, cols=None):
-    src = panel.cols if cols is None else cols
+    src = panel.values() if cols is None else cols
     sh = torch.empty((src.shape[0], panel.nseg), dtype=torch.float64, device=src.device)
     _kcall("fm_pilot_shift", "fm_pilot_shift", src.data_ptr(), src.stride(0), src.shape[0], panel.seg_off.data_ptr(),
            panel.nseg, sh.data_ptr(), _stream())
@@ -615,7 +732,7 @@ def _chunk_plan(panel: DevicePanel):
         seg, rows, off, wg = make_chunks_balanced(panel.seg_off_h, pol[1], panel.row_origin)
     else:
         seg, rows, off = make_chunks(panel.seg_off_h, pol[1])
-    dev = panel.cols.device
+    dev = panel.device
     t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     plan = _Plan(t(seg), t(rows), t(off), len(seg), t(order), t(wg), 0 if wg is None else len(wg) - 1)
     panel._chunk_cache = plan
@@ -693,7 +810,7 @@ def _solve_group(panel, src, gpl, partial, seg_chunk_off, zw, nlevels, T, pmax, 
         prob_model=gpl.pm.data_ptr(), prob_level=gpl.pl.data_ptr(), prob_z=gpl.pz.data_ptr(),
         prob_nz=gpl.pnz.data_ptr(), prob_flags=gpl.pf.data_ptr(), add_back=_ptr(add_back),
         gram_flags=None, nmodels=gpl.nmodels, pmax=pmax, rec=grec.data_ptr(),
-        status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride, ab_ncols=src.shape[0])
+        status=gst.data_ptr(), moments=_ptr(gmom), mom_stride=mom_stride, ab_ncols=src.ncols)
     # statsmodels fix-ups: the exact nonzero-constant test where the solve saw a near-zero
     # variance (CONST_SUSPECT), inf in y (pinv(X) @ y gives +-inf / NaN coefficients) and the
     # QR + SVD refit of ill-conditioned / rank-deficient problems (FM_ST_REFIT).  The 16-wide
@@ -701,16 +818,21 @@ def _solve_group(panel, src, gpl, partial, seg_chunk_off, zw, nlevels, T, pmax, 
     # the 32-wide one is followed by fm_solve_fixup, which scans the status on the device
     # (npairs = -1): no host round trip either way.
     inline_fix = zw == 16 and pmax + 1 <= 16
+    if not inline_fix and src.f64 is None:   # fm_solve_fixup reads FP64 columns
+        src = _source(panel, panel.values())
     if inline_fix:
-        sa.fix_cols, sa.fix_stride, sa.fix_seg_off = src.data_ptr(), src.stride(0), panel.seg_off.data_ptr()
+        # the fix-ups' rows: the FP64 columns, else the planes of a planes-only panel
+        sa.fix_cols, sa.fix_stride, sa.fix_seg_off = src.ptr, src.stride, panel.seg_off.data_ptr()
+        if src.f64 is None:
+            sa.fix_hi_plane, sa.fix_lo_plane = src.hp, src.lp
         sa.fix_lo, sa.fix_hi, sa.fix_shift, sa.fix_inv_scale = _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale)
         sa.fix_level, sa.fix_check_const = _ptr(level), int(bool(const_check))
     _kcall("fm_solve", "fm_solve", L.C.byref(sa), _stream())
-    _remember("fm_solve", "fm_solve", sa, partial, seg_chunk_off, gpl, add_back, grec, gst, gmom, src, lo, hi,
-              shift, inv_scale, level, *keep)
+    _remember("fm_solve", "fm_solve", sa, partial, seg_chunk_off, gpl, add_back, grec, gst, gmom, src.f64,
+              panel.planes, lo, hi, shift, inv_scale, level, *keep)
     if inline_fix:
         return grec, gst, gmom
-    _kcall("fm_solve_fixup", "fm_solve_fixup", src.data_ptr(), src.stride(0), panel.seg_off.data_ptr(), T,
+    _kcall("fm_solve_fixup", "fm_solve_fixup", src.ptr, src.stride, panel.seg_off.data_ptr(), T,
            _ptr(lo), _ptr(hi), _ptr(shift), _ptr(inv_scale), _ptr(add_back), _ptr(level), ng,
            gpl.pl.data_ptr(), gpl.pz.data_ptr(), gpl.pnz.data_ptr(), None, -1,
            gmom.data_ptr(), mom_stride, pmax, grec.data_ptr(), gst.data_ptr(), int(bool(const_check)),
@@ -732,8 +854,8 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
             shift=None, inv_scale=None, add_back=None, moments=False, cols=None, const_check=True):
     """One batched cross-sectional pass: every (model, universe level) problem for every
     month from one read of the panel per model group.  Returns an FMResult."""
-    src = panel.cols if cols is None else cols
-    ncols = src.shape[0]
+    src = _source(panel, cols)
+    ncols = src.ncols
     if ncols > L.FM_MAX_COLS:
         raise ValueError(f"at most {L.FM_MAX_COLS} columns per pass")
     dev = src.device
@@ -741,7 +863,7 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
     zw = 16 if ncols <= 15 else 32
     cap = 16 if zw == 16 else 8
     if shift is None:
-        shift = pilot_shift(panel, src)
+        shift = pilot_shift(panel, cols)
     if add_back is None and inv_scale is None:
         add_back = shift
     problems = _problems(models, nlevels)
@@ -760,22 +882,23 @@ def fm_pass(panel: DevicePanel, models: Sequence[Model], level=None, nlevels=1, 
         nb = gpl.npatterns * nlevels
         partial = torch.empty((plan.nchunks, nb, zw * (zw + 1) // 2), dtype=torch.float64, device=dev)
         flags = torch.empty((T, gpl.nmodels), dtype=torch.int32, device=dev)   # reserved: never read
-        ph, pl_, pst = _planes_for(panel, src)
         ga = L.GramArgs(
-            cols=src.data_ptr(), col_stride=src.stride(0), ncols=ncols, nseg=T,
+            cols=src.ptr, col_stride=src.stride if src.f64 is not None else 0, ncols=ncols, nseg=T,
             seg_off=panel.seg_off.data_ptr(), chunk_seg=plan.chunk_seg.data_ptr(),
             chunk_row=plan.chunk_row.data_ptr(), nchunks=plan.nchunks,
             lo=_ptr(lo), hi=_ptr(hi), shift=_ptr(shift), inv_scale=_ptr(inv_scale),
             level=_ptr(level), nlevels=nlevels, model_mask=gpl.mm.data_ptr(),
             model_ymask=gpl.ym.data_ptr(), nmodels=gpl.nmodels, pattern_id=gpl.lut.data_ptr(),
             npatterns=gpl.npatterns, partial=partial.data_ptr(), flags=flags.data_ptr(),
-            chunk_order=_ptr(plan.order), hi_plane=ph, lo_plane=pl_, plane_stride=pst,
+            chunk_order=_ptr(plan.order), hi_plane=src.hp, lo_plane=src.lp, plane_stride=src.pstride,
             wg_chunk_off=_ptr(plan.wg_off), nwg=plan.nwg)
         _kcall("fm_gram", "fm_gram", L.C.byref(ga), _stream())
-        _remember("fm_gram", "fm_gram", ga, src, partial, flags, lo, hi, shift, inv_scale, level, plan, gpl)
+        _remember("fm_gram", "fm_gram", ga, src.f64, panel.planes, partial, flags, lo, hi, shift, inv_scale, level,
+                  plan, gpl)
         grec, gst, gmom = _solve_group(panel, src, gpl, partial, plan.seg_chunk_off, zw, nlevels, T, pmax,
                                        mom_stride, lo, hi, shift, inv_scale, add_back, level,
-                                       const_check, (src, flags, lo, hi, shift, inv_scale, level, plan))
+                                       const_check, (src.f64, panel.planes, flags, lo, hi, shift, inv_scale,
+                                                     level, plan))
         if len(groups) == 1:
             rec, status = grec, gst
             mom = gmom if moments else None
@@ -1013,7 +1136,7 @@ def time_series_result(res: FMResult, nw_lags=4, window=120, min_periods=60, lag
 
 def forecast(panel: DevicePanel, coef, cols=None):
     """A7 per-row forecasts F = c0[t] + sum_k c_k[t] x_k for coef [T, K+1] (NaN propagates)."""
-    src = panel.cols if cols is None else cols
+    src = panel.values() if cols is None else cols
     coef = coef.contiguous()
     out = torch.empty(panel.nrows, dtype=torch.float64, device=src.device)
     _kcall("fm_forecast", "fm_forecast", src.data_ptr(), src.stride(0), src.shape[0], panel.seg_off.data_ptr(),
@@ -1023,7 +1146,7 @@ def forecast(panel: DevicePanel, coef, cols=None):
 
 def segment_moments(panel: DevicePanel, level=None, min_level=0, finite_only=True, cols=None):
     """Per (column, month) count, mean and ddof=1 std of the non-missing values."""
-    src = panel.cols if cols is None else cols
+    src = panel.values() if cols is None else cols
     C, T = src.shape[0], panel.nseg
     cnt = torch.empty((C, T), dtype=torch.int32, device=src.device)
     mean = torch.empty((C, T), dtype=torch.float64, device=src.device)

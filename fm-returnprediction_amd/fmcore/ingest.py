@@ -85,8 +85,10 @@ def arrow_host_columns(source, value_cols: Sequence[str], date_col: str = "mthca
 
 def panel_from_arrow(source, value_cols: Sequence[str], date_col: str = "mthcaldt",
                      me_col: Optional[str] = None, exch_col: Optional[str] = None,
-                     exch_value: str = "N", device=None) -> "E.DevicePanel":
-    """A pyarrow Table or a Parquet path -> month-sorted DevicePanel (one pinned H2D copy)."""
+                     exch_value: str = "N", device=None, layout="f64") -> "E.DevicePanel":
+    """A pyarrow Table or a Parquet path -> month-sorted DevicePanel (one pinned H2D copy),
+    in ``layout`` ("f64"; "planes": the split high / low-word layout only, gathered from the
+    raw words on the device; "both")."""
     import pyarrow.compute as pc
     import torch
     device = device or E.require_device()
@@ -108,13 +110,15 @@ def panel_from_arrow(source, value_cols: Sequence[str], date_col: str = "mthcald
     C = len(value_cols)
     raw = stage.to(device, non_blocking=True)
     perm = torch.from_numpy(order.astype(np.int64)).to(device, non_blocking=True)
-    cols = raw[:C].index_select(1, perm).contiguous()
+    cols, planes = E.gather_layout(raw[:C], perm, layout)
     me_t = raw[C].index_select(0, perm) if me_col else None
     nyse_t = None
     if nyse is not None:
         nyse_t = torch.from_numpy(nyse).to(device).index_select(0, perm)
     panel = E.DevicePanel(cols=cols, names=list(value_cols),
                           seg_off=torch.from_numpy(seg_off).to(device), seg_off_h=seg_off,
-                          months=uniq, me=me_t, nyse=nyse_t, order=order)
+                          months=uniq, me=me_t, nyse=nyse_t, order=order, planes=planes)
+    if cols is not None and planes is not None:
+        panel.planes_version = cols._version
     torch.cuda.current_stream().synchronize()   # the pinned stage must outlive the copy
     return panel

@@ -349,7 +349,7 @@ def build_table_1(subsets_crsp_comp: dict, variables_dict: dict) -> pd.DataFrame
                 am, _, _, an = _api.records_summary_device(vals, nw_lags=0)
             else:
                 am, an = np.full(2 * C, np.nan), np.zeros(2 * C, dtype=np.int64)
-            dev = panel.cols.device
+            dev = panel.device
             allv = torch.from_numpy(np.stack(arrays)).to(dev)                # every row, NaT months too
             ids = torch.from_numpy(df_subset["permno"].to_numpy(dtype=np.int64)).to(dev)
             nuniq = _E.distinct_count(ids, allv, finite_only=True).cpu().numpy()
@@ -406,7 +406,7 @@ def _fm_summaries(df, model_cols, level=None, nlevels=1, fig1=False, moments=Fal
     lvl_t = None
     if level is not None:
         import torch
-        lvl_t = torch.from_numpy(np.ascontiguousarray(level[panel.order])).to(panel.cols.device)
+        lvl_t = torch.from_numpy(np.ascontiguousarray(level[panel.order])).to(panel.device)
     levels = tuple(range(nlevels))
     models = [_E.Model(n, y=panel.col("retx"), xs=[panel.col(c) for c in xs], levels=levels)
               for n, xs in model_cols.items()]
@@ -610,7 +610,7 @@ def expected_return_forecasts(df: pd.DataFrame, coef_rolling: pd.DataFrame, pred
     arrays = [_api.as_f64(df[c]) for c in predictor_cols]
     panel = _E.panel_from_arrays(arrays, predictor_cols, df[date_col].values)
     c = coef_rolling[["const"] + predictor_cols].reindex(pd.Index(panel.months))
-    coef = torch.from_numpy(np.ascontiguousarray(c.to_numpy(dtype=np.float64))).to(panel.cols.device)
+    coef = torch.from_numpy(np.ascontiguousarray(c.to_numpy(dtype=np.float64))).to(panel.device)
     f = _E.forecast(panel, coef).cpu().numpy()
     out = np.full(len(df), np.nan)
     out[panel.order] = f

@@ -122,9 +122,9 @@ typedef struct fm_gram_args {
                                      reverse index order (the months fm_select streamed last, still
                                      in the Infinity Cache, first).  Only the launch order: each
                                      chunk's partial is the same either way */
-    /* optional: cols as 32-bit planes (fm_split_planes, [ncols][plane_stride] each): rows are
-     * read from the planes instead of cols (the same bytes; the high plane fm_select just
-     * streamed is still in the Infinity Cache).  NULL: cols */
+    /* optional: cols as 32-bit planes (fm_split_planes / fm_gen_panel_planes, [ncols][plane_stride]
+     * each): rows are read from the planes instead of cols (the same bytes; the high plane
+     * fm_select just streamed is still in the Infinity Cache), and cols may be NULL.  NULL: cols */
     const uint32_t* hi_plane;
     const uint32_t* lo_plane;
     int64_t plane_stride;
@@ -177,6 +177,10 @@ typedef struct fm_solve_args {
     const uint8_t* fix_level;
     int32_t fix_check_const;
     int32_t fix_pad;
+    /* the fix-ups' rows from the split panel's planes instead (fix_cols NULL; plane stride =
+     * fix_stride): a panel that holds no FP64 columns */
+    const uint32_t* fix_hi_plane;
+    const uint32_t* fix_lo_plane;
 } fm_solve_args;
 
 const char* fm_version(void);
@@ -241,6 +245,11 @@ typedef struct fm_select_args {
                                     long-month kernels then order values by these words (half the
                                     bytes) and gather full values from cols only at the target ranks */
     int64_t plane_stride;
+    const uint32_t* lo_plane;    /* optional, with hi_plane: the low words.  With both planes cols may
+                                    be NULL (a split panel without FP64 columns): the gathers and the
+                                    fix-up paths then read values from the planes.  Paths that need
+                                    FP64 columns (moments, row masks, > 20,480-row months) return
+                                    FM_EINVAL for such a panel. */
 } fm_select_args;
 
 int fm_select(const fm_select_args* args, void* stream);
@@ -475,6 +484,19 @@ int fm_rolling_beta(const int32_t* day, const double* ri, const double* rm, int6
 int fm_gen_panel(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
                  double nan_rate, double nyse_rate, double* cols, int64_t col_stride,
                  double* me, uint8_t* nyse, void* stream);
+
+/* fm_gen_panel writing the split layout directly: the values' high / low 32-bit words into
+ * hi / lo ([ncols][plane_stride]), the FP64 columns into cols too when cols != NULL (else
+ * not at all).  The same values as fm_gen_panel bit for bit; no separate layout pass. */
+int fm_gen_panel_planes(uint64_t seed, int64_t month0, int32_t nmonths, int32_t nfirms,
+                        double nan_rate, double nyse_rate, double* cols, int64_t col_stride,
+                        uint32_t* hi, uint32_t* lo, int64_t plane_stride, double* me, uint8_t* nyse,
+                        void* stream);
+
+/* The inverse of fm_split_planes: FP64 columns from the two planes (for consumers of a split
+ * panel that read FP64 columns: clip, forecasts, Table 1, moments). */
+int fm_merge_planes(const uint32_t* hi, const uint32_t* lo, int64_t plane_stride, int32_t ncols, int64_t nrows,
+                    double* cols, int64_t col_stride, void* stream);
 
 /* The FP64 columns as two 32-bit planes: hi[c][r] / lo[c][r] = the high / low words of
  * cols[c][r] (plane_stride >= nrows).  The split panel's hi plane feeds fm_select_args.hi_plane

@@ -1637,3 +1637,89 @@ def test_split_month_gram_plan_matches_whole(E):
         for k in range(ra.shape[1]):
             for j in range(ra.shape[2] - 1):
                 assert_series_close(rb[:, k, j], ra[:, k, j], f"{plan} problem {k} col {j}", rtol=1e-12)
+
+
+# ---------------------------------------------------------------- planes-only panels (round 6)
+def _pipe_host(out):
+    d = {"rec": out.res.rec, "status": out.res.status, "mean": out.summary.mean, "se": out.summary.se,
+         "t": out.summary.tstat, "nobs": out.summary.nobs, "lo": out.cuts.lo, "hi": out.cuts.hi,
+         "nvalid": out.cuts.nvalid, "center": out.cuts.center, "level": out.level,
+         "bp_a": out.breakpoints[0], "bp_b": out.breakpoints[1], "pred": out.pred, "pst": out.pred_status,
+         "pmean": out.pred_summary.mean, "ptstat": out.pred_summary.tstat}
+    return {k: v.cpu().numpy() for k, v in d.items()}
+
+
+@pytest.mark.parametrize("shape", [(60, 5000), (12, 20000)])
+def test_planes_only_panel_pipeline_bit_identical(E, shape):
+    """A panel generated straight into the split layout (fm_gen_panel_planes: high / low
+    32-bit planes, NO FP64 columns) gives the Table-2 / Figure-1 pass of the FP64 panel bit
+    for bit: cuts (signs of the dy column's exactly-zero 1% cuts included: their replay reads
+    the planes), universes, records, status, summaries, predictive records.  Short months (the
+    two-wave select) and C5-length 20,000-row months (the long-month high-key kernel, whose
+    candidate gathers read the planes)."""
+    from fmcore import lewellen as LW
+    T, N = shape
+    pa = E.panel_synthetic(T, N, 9, layout="f64")
+    pb = E.panel_synthetic(T, N, 9, layout="planes")
+    assert pb.cols is None and pb.planes is not None
+    cfg = LW.PipelineConfig()
+    a = _pipe_host(LW.run_pipeline(pa, cfg))
+    b = _pipe_host(LW.run_pipeline(pb, cfg))
+    assert pb.cols is None and "_merged" not in pb.__dict__   # the pass never asked for FP64 columns
+    for k in a:
+        if a[k].dtype.kind == "f":
+            assert _same(b[k], a[k]), k
+        else:
+            assert np.array_equal(b[k], a[k]), k
+    # the generator's planes are the FP64 values' words
+    ha = pa.cols.cpu().numpy().view(np.uint64)
+    hb = (pb.planes[0].cpu().numpy().astype(np.uint32).astype(np.uint64) << np.uint64(32)) | \
+        pb.planes[1].cpu().numpy().astype(np.uint32).astype(np.uint64)
+    assert np.array_equal(ha, hb)
+
+
+def test_planes_only_panel_fixup_paths(E):
+    """The rare select / solve paths on a planes-only panel read values through the planes:
+    pct.npz (+-inf, NaN runs, ties, signed zeros: units marked for the workgroup fix-up and
+    zero-cut sign replays) from panel_from_arrays(layout="planes") gives the FP64 panel's cuts
+    bit for bit; a near-collinear model (x2 = x1 + 1e-8 noise: FM_ST_REFIT months re-solved
+    from the rows by the solve's inline QR + SVD refit) the same records and status."""
+    g = load_npz("pct.npz")
+    vals, off, qs = g["values"], g["offsets"], g["qs"]
+    labels = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    pf = E.panel_from_arrays([vals], ["v"], labels)
+    pp = E.panel_from_arrays([vals], ["v"], labels, layout="planes")
+    assert pp.cols is None
+    for a, b in [(0, 1), (2, 3), (4, 5), (6, 6)]:
+        cf = E.select_cuts(pf, qs[a] / 100, qs[b] / 100, 1, E.LERP_NUMPY, center=True)
+        cp = E.select_cuts(pp, qs[a] / 100, qs[b] / 100, 1, E.LERP_NUMPY, center=True)
+        for f in ("lo", "hi", "center"):
+            assert _same(getattr(cp, f).cpu().numpy(), getattr(cf, f).cpu().numpy()), (qs[a], f)
+        assert np.array_equal(cp.nvalid.cpu().numpy(), cf.nvalid.cpu().numpy())
+    df = cases._edge_base(8, 300, 4, 77)
+    rng = np.random.default_rng(78)
+    df["x2"] = df["x1"] + 1e-8 * rng.standard_normal(len(df))
+    names = ["retx", "x0", "x1", "x2", "x3"]
+    labels = df["mthcaldt"].values
+    out = {}
+    for layout in ("f64", "planes"):
+        p = E.panel_from_arrays([df[c].values for c in names], names, labels, layout=layout)
+        m = E.Model("m", y=0, xs=[1, 2, 3, 4])
+        cuts = E.select_cuts(p, 0.01, 0.99, 5, E.LERP_NUMPY, center=True)
+        res = E.fm_pass(p, [m], cuts=cuts, shift=cuts.center, moments=True)
+        out[layout] = (res.rec.cpu().numpy(), res.status.cpu().numpy())
+    st = out["f64"][1]
+    assert ((st & E.L.FM_ST_REFIT) != 0).any(), "the case must take the refit path"
+    assert _same(out["planes"][0], out["f64"][0]) and np.array_equal(out["planes"][1], st)
+
+
+def test_planes_stale_after_in_place_write_refused(E):
+    """A panel holding both layouts refuses to run once its FP64 columns were written in
+    place after the planes were made (the planes would be stale); split_planes re-arms it."""
+    p = E.panel_synthetic(4, 300, 2, layout="both")
+    E.select_cuts(p, 0.01, 0.99, 5, E.LERP_NUMPY)
+    p.cols[0, 0] = 1.0
+    with pytest.raises(RuntimeError, match="modified in place"):
+        E.select_cuts(p, 0.01, 0.99, 5, E.LERP_NUMPY)
+    E.split_planes(p)
+    E.select_cuts(p, 0.01, 0.99, 5, E.LERP_NUMPY)
