@@ -37,15 +37,27 @@ constexpr int WAVE = 64;
 struct PCols {
     const double* f = nullptr;
     const uint32_t* h = nullptr;
-    const uint32_t* l = nullptr;
+    int64_t loff = 0;   // the low plane at this element offset from the high one
     __device__ __forceinline__ double operator[](int64_t i) const {
         if (f != nullptr) return f[i];
-        return __longlong_as_double((long long)(((uint64_t)h[i] << 32) | l[i]));
+        return __longlong_as_double((long long)(((uint64_t)h[i] << 32) | h[i + loff]));
     }
     __device__ __forceinline__ PCols off(int64_t o) const {
-        return f != nullptr ? PCols{f + o, nullptr, nullptr} : PCols{nullptr, h + o, l + o};
+        return f != nullptr ? PCols{f + o, nullptr, 0} : PCols{nullptr, h + o, loff};
     }
-    __host__ __device__ __forceinline__ bool valid() const { return f != nullptr || (h != nullptr && l != nullptr); }
+};
+// The same two views as separate types, for code that is instantiated per layout (a branch
+// per access inside a register-heavy unrolled loop costs registers: the solve's fix-ups)
+struct F64Cols {
+    const double* f;
+    __device__ __forceinline__ double operator[](int64_t i) const { return f[i]; }
+};
+struct PlaneCols {   // the low plane at a fixed element offset from the high one (one base pointer)
+    const uint32_t* h;
+    int64_t loff;
+    __device__ __forceinline__ double operator[](int64_t i) const {
+        return __longlong_as_double((long long)(((uint64_t)h[i] << 32) | h[i + loff]));
+    }
 };
 
 // Phase probe (timing builds only, tools/build_variant.sh probe "-DFM_PROBE=1" ...;

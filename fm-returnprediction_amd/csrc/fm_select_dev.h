@@ -92,9 +92,8 @@ struct SelArgs {
 
 // Column c of the panel from row r0 on, as FP64 values or from the two planes
 __device__ __forceinline__ PCols sel_col(const SelArgs& a, int c, int64_t r0) {
-    if (a.cols != nullptr) return PCols{a.cols + (int64_t)c * a.col_stride + r0, nullptr, nullptr};
-    const int64_t o = (int64_t)c * a.pstride + r0;
-    return PCols{nullptr, a.hp + o, a.lp + o};
+    if (a.cols != nullptr) return PCols{a.cols + (int64_t)c * a.col_stride + r0, nullptr, 0};
+    return PCols{nullptr, a.hp + (int64_t)c * a.pstride + r0, (int64_t)(a.lp - a.hp)};
 }
 
 // One lane: unit u goes on the fix-up kernel's worklist (and is marked, nvalid = -1, when the

@@ -392,8 +392,8 @@ constexpr int G16 = 16;   // lanes per problem
 template <int NC, int NT>
 union FixSmem;
 inline __device__ bool fix_wanted(uint32_t st, int check_const);
-template <int NC, int NT>
-__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, PCols cols, int64_t stride,
+template <int NC, int NT, class CA>
+__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, CA cols, int64_t stride,
                         const int64_t* seg_off, int nseg, const double* lo, const double* hi,
                         const double* shift, const double* inv_scale, const double* add_back,
                         const uint8_t* level, int nprob, const int32_t* prob_level, const int32_t* prob_z,
@@ -407,7 +407,7 @@ __device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, N
 constexpr int S16T = 192;
 constexpr int S16W = S16T / WAVE;
 constexpr int S16_MAXP = 32;   // problems per group held in LDS tables
-__global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
+__global__ __launch_bounds__(S16T, 3) void solve16_kernel(fm_solve_args a) {
     extern __shared__ double bs[];   // [nb][136] packed bucket sums of this month
     // per wave: four transpose tiles, or (afterwards, one problem at a time) the Jacobi
     // fallback's scratch (a union)
@@ -695,25 +695,28 @@ __global__ __launch_bounds__(S16T, 2) void solve16_kernel(fm_solve_args a) {
     FM_PROBE_AT(solve, 3);
     // the statsmodels fix-ups of this month's flagged problems (fm_solve_fixup's work, rare),
     // by this workgroup: its own rec / moments / status writes are visible after the barrier
-    const PCols fcols{a.fix_cols, a.fix_hi_plane, a.fix_lo_plane};
-    if (fcols.valid()) {   // block-uniform
+    // the rows come from the FP64 columns, else (a planes-only panel) from the two planes: one
+    // instantiation per layout (a per-access branch raised the kernel to 231 VGPRs)
+    auto fix_all = [&](auto cols) {
         __syncthreads();
         const int ckc = a.fix_check_const;
         for (int q = 0; q < a.nprob; ++q) {
             const uint32_t st = t_st[q];
             if (!fix_wanted(st, ckc)) continue;   // block-uniform
-            fix_one<G16, S16T>(s, q, st, *reinterpret_cast<FixSmem<G16, S16T>*>(&wsc[0][0]), fcols,
+            fix_one<G16, S16T>(s, q, st, *reinterpret_cast<FixSmem<G16, S16T>*>(&wsc[0][0]), cols,
                                a.fix_stride, a.fix_seg_off, a.nseg, a.fix_lo, a.fix_hi, a.fix_shift,
                                a.fix_inv_scale, a.add_back, a.fix_level, a.nprob, a.prob_level, a.prob_z,
                                a.prob_nz, a.moments, a.mom_stride, a.pmax, a.rec, a.status, ckc);
         }
-    }
+    };
+    if (a.fix_cols != nullptr) fix_all(F64Cols{a.fix_cols});   // block-uniform
+    else if (a.fix_hi_plane != nullptr) fix_all(PlaneCols{a.fix_hi_plane, (int64_t)(a.fix_lo_plane - a.fix_hi_plane)});
 }
 
 // Exact nonzero-constant test for problems flagged CONST_SUSPECT (statsmodels
 // add_constant(has_constant='skip'): np.ptp(x)==0 & all(x != 0), src/regressions.py:50).
-template <int NT = VT>
-__device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, PCols cols, int64_t stride,
+template <int NT = VT, class CA = F64Cols>
+__device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, CA cols, int64_t stride,
                                            const int64_t* seg_off, int nseg, const double* lo,
                                            const double* hi, const uint8_t* level, int nprob,
                                            const int32_t* prob_level, const int32_t* prob_z,
@@ -755,7 +758,7 @@ __device__ __forceinline__ void const_pair(int s, int p, uint64_t* red, PCols co
     if (threadIdx.x == 0 && any_const) status[(int64_t)s * nprob + p] |= FM_ST_CONST_COL;
 }
 
-__global__ __launch_bounds__(VT) void const_kernel(PCols cols, int64_t stride, int ncols,
+__global__ __launch_bounds__(VT) void const_kernel(F64Cols cols, int64_t stride, int ncols,
                                                    const int64_t* seg_off, int nseg,
                                                    const double* lo, const double* hi,
                                                    const uint8_t* level, int nprob,
@@ -793,8 +796,8 @@ struct InfySmem {
     int okf;
 };
 
-template <int NT = VT, int NC = 32>
-__device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, PCols cols, int64_t stride,
+template <int NT = VT, int NC = 32, class CA = F64Cols>
+__device__ __forceinline__ void infy_pair(int s, int p, InfySmem& sm, CA cols, int64_t stride,
                                           const int64_t* seg_off, int nseg, const double* lo,
                                           const double* hi, const double* shift,
                                           const double* inv_scale, const double* add_back,
@@ -1044,8 +1047,8 @@ __device__ __forceinline__ void hh_absorb(double (&a)[NC], double (*R)[NC + 1], 
     });
 }
 
-template <int NC, int NT = VT>
-__device__ void refit_pair(int s, int p, RefitSmem<NC, NT / WAVE>& sm, PCols cols, int64_t stride,
+template <int NC, int NT = VT, class CA = F64Cols>
+__device__ void refit_pair(int s, int p, RefitSmem<NC, NT / WAVE>& sm, CA cols, int64_t stride,
                            const int64_t* seg_off, int nseg, const double* lo, const double* hi,
                            const double* shift, const double* inv_scale, const double* add_back,
                            const uint8_t* level, int nprob, const int32_t* prob_level,
@@ -1203,8 +1206,8 @@ inline __device__ bool fix_wanted(uint32_t st, int check_const) {
 }
 // The fix-ups of one flagged (month, problem) whose solve status is `st`, by the whole
 // NT-thread workgroup (block-uniform; ends with the workgroup synchronized)
-template <int NC, int NT>
-__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, PCols cols,
+template <int NC, int NT, class CA>
+__device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, NT>& sm, CA cols,
                                         int64_t stride, const int64_t* seg_off, int nseg, const double* lo,
                                         const double* hi, const double* shift, const double* inv_scale,
                                         const double* add_back, const uint8_t* level, int nprob,
@@ -1230,7 +1233,7 @@ __device__ __forceinline__ void fix_one(int s, int p, uint32_t st, FixSmem<NC, N
 }
 
 template <int NC>
-__global__ __launch_bounds__(VT) void fixup_kernel(PCols cols, int64_t stride,
+__global__ __launch_bounds__(VT) void fixup_kernel(F64Cols cols, int64_t stride,
                                                    const int64_t* seg_off, int nseg, const double* lo,
                                                    const double* hi, const double* shift,
                                                    const double* inv_scale, const double* add_back,
@@ -1337,7 +1340,7 @@ extern "C" int fm_const_check(const double* cols, int64_t col_stride, int32_t nc
     const int64_t work = npairs < 0 ? (int64_t)nseg * nprob : npairs;
     if (work == 0) return FM_OK;
     const int grid = (int)(npairs < 0 ? (work < SCAN_GRID ? work : SCAN_GRID) : work);
-    hipLaunchKernelGGL(const_kernel, dim3(grid), dim3(VT), 0, (hipStream_t)stream, PCols{cols, nullptr, nullptr},
+    hipLaunchKernelGGL(const_kernel, dim3(grid), dim3(VT), 0, (hipStream_t)stream, F64Cols{cols},
                        col_stride, ncols, seg_off, nseg, lo, hi, level, nprob, prob_level, prob_z,
                        prob_nz, pairs, npairs, status);
     FM_CHECK_LAUNCH("fm_const_check");
@@ -1362,11 +1365,11 @@ extern "C" int fm_solve_fixup(const double* cols, int64_t col_stride, const int6
     const int64_t ranges = (work + VT - 1) / VT;   // VT pairs per workgroup pass
     const int grid = (int)(ranges < SCAN_GRID ? ranges : SCAN_GRID);
     if (pmax + 1 <= 16)
-        hipLaunchKernelGGL(fixup_kernel<16>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, PCols{cols, nullptr, nullptr},
+        hipLaunchKernelGGL(fixup_kernel<16>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, F64Cols{cols},
                            col_stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
                            prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status, check_const);
     else
-        hipLaunchKernelGGL(fixup_kernel<32>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, PCols{cols, nullptr, nullptr},
+        hipLaunchKernelGGL(fixup_kernel<32>, dim3(grid), dim3(VT), 0, (hipStream_t)stream, F64Cols{cols},
                            col_stride, seg_off, nseg, lo, hi, shift, inv_scale, add_back, level, nprob, prob_level,
                            prob_z, prob_nz, pairs, npairs, moments, mom_stride, pmax, rec, status, check_const);
     FM_CHECK_LAUNCH("fm_solve_fixup");

@@ -17,7 +17,8 @@ def child():
     from fmcore import engine as E
     from fmcore import lewellen as LW
     dev = E.require_device()
-    panel = E.panel_synthetic(600, 5000, 1, device=dev)
+    # KB_PLANES=2: the planes-only panel bench.py times (fm_gen_panel_planes, no FP64 columns)
+    panel = E.panel_synthetic(600, 5000, 1, device=dev, layout="planes" if os.environ.get("KB_PLANES") == "2" else "f64")
     if os.environ.get("KB_CHUNK"):   # Gram chunk-size A/B (rows per workgroup)
         panel.chunk_rows = int(os.environ["KB_CHUNK"])
     pol = os.environ.get("KB_POLICY", "")
@@ -26,7 +27,7 @@ def child():
     if os.environ.get("KB_SLOTS"):   # the balanced plan cut for this many workgroups
         panel.chunk_policy = E.chunk_policy(panel.nrows, panel.nseg, panel.max_seg_len, slots=int(os.environ["KB_SLOTS"]))
 
-    if os.environ.get("KB_PLANES") == "1":   # the split panel (fm_split_planes)
+    if os.environ.get("KB_PLANES") == "1":   # FP64 columns + the split planes (fm_split_planes)
         E.split_planes(panel)
     cfg = LW.PipelineConfig()
     for _ in range(3):
