@@ -25,6 +25,7 @@ for s in "$@"; do
     wgtime)  specs+=("wgtime:::200:::FM_HIP_LIB=$R/build_variants/wgtime/libfm_hip.so python tools/gram_wgtime.py");;
     kbench)  specs+=("kbench:::300:::python tools/kbench.py $KB_LIBS");;
     slab)    specs+=("slab:::300:::python tools/slab_probe.py");;
+    cacheab) specs+=("cacheab:::300:::python tools/cache_ab.py");;
     selbench) specs+=("selbench:::300:::python tools/selbench.py $KB_LIBS");;
     stdbench) specs+=("stdbench:::300:::python tools/stdbench.py $KB_LIBS");;
     kstats)  specs+=("kstats:::500:::$PROF --kernel-trace --stats -d $R/gpurun_out/kt -o kt --output-format csv -- python3 $R/bench.py --no-cpu --no-chars --steps 10 $BENCH_ARGS");;
