@@ -38,7 +38,7 @@ __device__ uint32_t g_wgtime[4 * WGT_MAX];   // the probe's own buffer, bounds-c
 // One workgroup per chunk (normally a whole month: the chunk plan makes chunks as large as
 // the chip's resident workgroup slots allow, so the prologue and the cross-wave epilogue run
 // once per month and every wave streams ~20 tiles back to back).  MINW = waves per SIMD.
-template <int NT, int NB, int MINW, bool PL>
+template <int NT, int NB, int MINW, bool PL, bool FULLC>
 __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
     using S = GramShape<NT>;
     __shared__ double tile[GNW * S::WT];
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
             const double dflt = kind < 2 ? NAN : (kind == 2 ? 0.0 : 1.0);
             pv = on ? v : dflt;
         }
-        GramWave<NT, NB, GNW, PL> g(a, r0, r1, w);
+        GramWave<NT, NB, GNW, PL, FULLC> g(a, r0, r1, w);
         g.prefetch();
         if (chunk == c0) {
             for (int e = tid; e < 4 * S::RS; e += GT) zblk[e] = 0.0;
@@ -111,10 +111,17 @@ __global__ __launch_bounds__(GT, MINW) void gram_kernel(fm_gram_args a) {
 template <int NT, int NB, int MINW>
 void launch_gram(const fm_gram_args& a, hipStream_t st) {
     const int grid = a.wg_chunk_off != nullptr ? a.nwg : a.nchunks;
-    if (a.hi_plane != nullptr)
-        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true>), dim3(grid), dim3(GT), 0, st, a);
-    else
-        hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false>), dim3(grid), dim3(GT), 0, st, a);
+    // ncols == ZW - 1 (the Table-2 panel's 15 columns): the row loads step through the columns
+    // without the "past ncols" test (the Gram's scalar stream had 4 instructions per column
+    // and plane for it)
+    const bool full = a.ncols == 16 * NT - 1;
+    if (a.hi_plane != nullptr) {
+        if (full) hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true, true>), dim3(grid), dim3(GT), 0, st, a);
+        else hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, true, false>), dim3(grid), dim3(GT), 0, st, a);
+    } else {
+        if (full) hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false, true>), dim3(grid), dim3(GT), 0, st, a);
+        else hipLaunchKernelGGL((gram_kernel<NT, NB, MINW, false, false>), dim3(grid), dim3(GT), 0, st, a);
+    }
 }
 
 }  // namespace

@@ -109,7 +109,7 @@ struct GramShape {
 //   ... fill the month parameters (prm) / pattern table (lut) / zero rows, barrier ...
 //   g.run(prm, lut, scaled, tile, zblk);  barrier-free per wave
 //   g.epilogue(tile, outp);   (all waves: cross-wave sum + packed store, barriers inside)
-template <int NT, int NB, int NWV, bool PL = false>
+template <int NT, int NB, int NWV, bool PL = false, bool FULLC = false>
 struct GramWave {
     using S = GramShape<NT>;
     static constexpr int ZW = S::ZW, RS = S::RS, TR = S::TR, WT = S::WT, PK = S::PK, NI = S::NI;
@@ -162,7 +162,9 @@ struct GramWave {
                 const uint32_t h = *(const __attribute__((address_space(1))) uint32_t*)((gptr)hb + lo * 4u);
                 const uint32_t l = *(const __attribute__((address_space(1))) uint32_t*)((gptr)lb + lo * 4u);
                 xv[c] = __longlong_as_double((long long)(((uint64_t)h << 32) | l));
-                const int64_t step = c + 1 < a.ncols ? a.plane_stride : 0;
+                // FULLC (ncols == ZW - 1, the Table-2 panel): every column step is the stride --
+                // no per-column compare and selects in the scalar stream
+                const int64_t step = FULLC || c + 1 < a.ncols ? a.plane_stride : 0;
                 hb += step;
                 lb += step;
                 asm("" : "+s"(hb), "+s"(lb));
@@ -171,7 +173,7 @@ struct GramWave {
 #pragma unroll
             for (int c = 0; c < ZW - 1; ++c) {
                 xv[c] = *(const __attribute__((address_space(1))) double*)((gptr)cb + lo * 8u);
-                cb += c + 1 < a.ncols ? a.col_stride : 0;   // columns past ncols re-read the last
+                cb += FULLC || c + 1 < a.ncols ? a.col_stride : 0;   // columns past ncols re-read the last
                 // opaque to the optimizer: otherwise it turns a repeated address into a register
                 // copy of the previous load behind a branch, i.e. a vmcnt(0) wait per column
                 asm("" : "+s"(cb));
@@ -333,18 +335,22 @@ struct GramWave {
 #pragma unroll
                     for (int i = 0; i < KB; ++i) mb &= ((b >> i) & 1) ? bit[i] : ~bit[i];
                     const int n = (int)__popcll(mb);
-                    for (int g = 0; g < n; g += 4) {
-                        const double Ar = An;
+                    // one 4-row group: operand `cur` (read one group ahead), the next group's
+                    // read into `nxt`.  Rows past the tile end (rn + kr <= TR + 3: lanes of rows
+                    // past a bucket's count) read this wave's own TPAD pad rows, never another
+                    // wave's tile; their (unwritten) values are masked here
+                    auto group = [&](int g, const double cur, double& nxt) {
                         const int rn = g + 4 < n ? off + g + 4 : off + n;
-                        // rows past the tile end (rn + kr <= TR + 3: lanes of rows past a
-                        // bucket's count) read this wave's own TPAD pad rows, never another
-                        // wave's tile; their (unwritten) values are masked below
-                        An = rd[rn * RS];
-                        const double A = kr < n - g ? Ar : 0.0;
+                        nxt = rd[rn * RS];
+                        const double A = kr < n - g ? cur : 0.0;
                         const double B1 = dpp_f64<0x12C>(A), B2 = dpp_f64<0x128>(A);
                         acc[b][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, A, acc[b][0], 0, 0, 0);
                         acc[b][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, B1, acc[b][1], 0, 0, 0);
                         acc[b][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(A, B2, acc[b][2], 0, 0, 0);
+                    };
+                    for (int g = 0; g < n; g += 4) {
+                        const double Ar = An;
+                        group(g, Ar, An);
                     }
                     off += n;
                 }
