@@ -1091,7 +1091,12 @@ def test_pipeline_c5_rank_shard_full_size(E):
     import torch
     from fmcore import lewellen as LW
     T, N, seed, m0 = 12500, 20000, 20150101, 50000
-    panel = E.panel_synthetic(T, N, seed, month0=m0)
+    # the layout bench.py's C5 shard uses: the split planes only (no FP64 columns), 30 GB of
+    # values for the 250M x 15 panel, 32.25 GB with me / NYSE (round 5 held 60 GB)
+    panel = E.panel_synthetic(T, N, seed, month0=m0, layout="planes")
+    assert panel.cols is None
+    held = sum(t.numel() * t.element_size() for t in (panel.planes, panel.me, panel.nyse, panel.seg_off))
+    assert held <= 32.3e9, held
     cfg = LW.PipelineConfig()
     assert not E.ts_fused_fits(T, 16, cfg.window, cfg.lag, predictive=True)
     out = LW.run_pipeline(panel, cfg)
@@ -1099,6 +1104,7 @@ def test_pipeline_c5_rank_shard_full_size(E):
     _check_records_vs_oracle(out.res, out.model_names, (0, 1, T // 2, T - 1), N, seed, m0)
     assert ((out.res.status.cpu().numpy() & 1) != 0).all()
     _check_series_vs_restatement(out.res, out.summary, out.rolling, cols=2)
+    assert "_merged" not in panel.__dict__   # the pass never materialized FP64 columns
 
 
 def _check_records_vs_oracle(res, names, months, N, seed, m0=0):
@@ -1183,6 +1189,11 @@ def test_pipeline_headline_panel_full_size(E):
     step = ShardedStep(panel, cfg, LW.table2_models())
     gres, summ, psumm = step.eager()
     assert _same(gres.rec.cpu().numpy(), flat_rec)
+    # the panel exactly as bench.py generates it: the planes only (fm_gen_panel_planes)
+    pp = E.panel_synthetic(T, N, seed, layout="planes")
+    pres, _, ppsumm = ShardedStep(pp, cfg, LW.table2_models()).eager()
+    assert _same(pres.rec.cpu().numpy(), flat_rec)
+    del pp, pres
     step.capture()
     ggres, gsumm, gpsumm = step.replay()
     torch.cuda.synchronize()
