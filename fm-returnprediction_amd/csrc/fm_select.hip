@@ -732,6 +732,12 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
 // wrap past the top).  The one thing a high word cannot tell is +-inf from a NaN whose payload
 // is all in the low word (high word 0x7FF00000 / 0xFFF00000): units holding either key
 // (thread min 0 / thread max HK_MAX) are marked and redone by the exact streaming kernel.
+#ifndef FM_HK_ABL
+#define FM_HK_ABL 0   // timing ablations only (wrong cuts): 1 = stop after the thresholds, 2 = before the gather, 3 = after the counts
+#endif
+#ifndef FM_HK_WAVELIST
+#define FM_HK_WAVELIST 1   // long-month candidates written straight into per-wave runs (no count pass)
+#endif
 #ifndef FM_HK_RIDE
 #define FM_HK_RIDE 1   // a universe rides the high-key kernel's launch (one more grid column)
 #endif
@@ -758,32 +764,64 @@ struct LongHkSmem {
     uint64_t res[4];
 };
 
-// The high words of a unit into hk (raw; hkey is applied by the unit's own pass): buffer
-// loads, one descriptor per slot of LT rows (scalar), the lane's byte offset the only VGPR;
-// rows past the month end read 0 through the descriptor's range check (masked later).
+// The high words of a unit into hk (raw; hkey is applied by the unit's own pass).  Slot v of
+// thread t holds row hk_row(v, t): with FM_HK_X4, four consecutive rows per 16-byte load
+// (row 4 LT (v / 4) + 4 t + v % 4: one descriptor per unit, a quarter of the load issue);
+// otherwise row LT v + t, one 4-byte load per slot.  Rows past the month end read 0 through
+// the descriptor's range check (checked per dword; masked later).
+#ifndef FM_HK_X4
+#define FM_HK_X4 1
+#endif
+__device__ __forceinline__ int hk_row(int v, int t) {
+    return FM_HK_X4 ? (v >> 2) * (4 * LT) + 4 * t + (v & 3) : v * LT + t;
+}
+
 template <int VPT>
 __device__ __forceinline__ void hk_load(const double* col, int L, uint32_t (&hk)[VPT]) {
-    const uint32_t lb = (uint32_t)threadIdx.x * 8u + 4u;   // little-endian: byte 4 = high word
+    if constexpr (FM_HK_X4) {
+        static_assert(VPT % 4 == 0, "hk_load: 16-byte slots");
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)col, 0, L * 8, 0x00020000);
+        const uint32_t lb = (uint32_t)threadIdx.x * 32u + 4u;   // little-endian: byte 4 = high word
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-        const int rem = L - v * LT;   // rows from this slot's first row to the month end
-        const int nrec = rem > 0 ? (rem < LT ? rem : LT) * 8 : 0;
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(col + (rem > 0 ? v * LT : 0)), 0, nrec,
-                                                          0x00020000);
-        hk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb, 0, 0);
+        for (int v = 0; v < VPT; ++v)
+            hk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb + (uint32_t)(v & 3) * 8u,
+                                                                  (v >> 2) * (4 * LT * 8), 0);
+    } else {
+        const uint32_t lb = (uint32_t)threadIdx.x * 8u + 4u;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            const int rem = L - v * LT;   // rows from this slot's first row to the month end
+            const int nrec = rem > 0 ? (rem < LT ? rem : LT) * 8 : 0;
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(col + (rem > 0 ? v * LT : 0)), 0, nrec,
+                                                              0x00020000);
+            hk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb, 0, 0);
+        }
     }
 }
 
 // ... or from the high-word plane (4 bytes per value read instead of 8)
 template <int VPT>
 __device__ __forceinline__ void hk_load_plane(const uint32_t* hp, int L, uint32_t (&hk)[VPT]) {
-    const uint32_t lb = (uint32_t)threadIdx.x * 4u;
+    if constexpr (FM_HK_X4) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)hp, 0, L * 4, 0x00020000);
+        const uint32_t lb = (uint32_t)threadIdx.x * 16u;
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-        const int rem = L - v * LT;
-        const int nrec = rem > 0 ? (rem < LT ? rem : LT) * 4 : 0;
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(hp + (rem > 0 ? v * LT : 0)), 0, nrec, 0x00020000);
-        hk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb, 0, 0);
+        for (int v = 0; v < VPT / 4; ++v) {
+            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, lb, v * (4 * LT * 4), 0);
+            hk[4 * v] = q[0];
+            hk[4 * v + 1] = q[1];
+            hk[4 * v + 2] = q[2];
+            hk[4 * v + 3] = q[3];
+        }
+    } else {
+        const uint32_t lb = (uint32_t)threadIdx.x * 4u;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+            const int rem = L - v * LT;
+            const int nrec = rem > 0 ? (rem < LT ? rem : LT) * 4 : 0;
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(hp + (rem > 0 ? v * LT : 0)), 0, nrec, 0x00020000);
+            hk[v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, lb, 0, 0);
+        }
     }
 }
 
@@ -798,9 +836,9 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
     const PCols col = sel_col(a, c, r0);
     // rows past the month end (read as 0 by the range check) -> HK_NONE; straight-line (a
     // scalar branch per slot split the block and pushed keys into scratch)
-    const int lim = L - tid;
+    const int lim = L - hk_row(0, tid);
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) hk[v] = v * LT < lim ? hkey(hk[v]) : HK_NONE;
+    for (int v = 0; v < VPT; ++v) hk[v] = hk_row(v, 0) < lim ? hkey(hk[v]) : HK_NONE;
     // count of valid values (ballots: scalar counts), thread min key and max key (NaN keys are
     // above HK_MAX for the min; +0x1FFFFE moves them below every valid key for the max)
     int cw = 0;
@@ -829,10 +867,15 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
     bool ok = (packed >> 16) == 0;
     // phases: thresholds + compaction (cand), then ONE site that gathers the candidates and
     // issues the next unit's loads (every path reaches it), then the sort / merge
-    bool cand = false;
+    bool cand = false, fast_done = false;   // fast_done: the candidates are in per-wave runs
     int i0 = 0, j0 = 0, i1 = 0, j1 = 0, clo = 0, chi = 0;
     double g0 = 0.0, g1 = 0.0;
+#if FM_HK_ABL == 3
+    lo = -1.0; hi = 1.0;
+    if (false) {
+#else
     if (ok && n >= a.min_count && n > 0) {   // block-uniform
+#endif
         qranks(n, a.q_lo, a.lerp_mode, i0, j0, g0);
         qranks(n, a.q_hi, a.lerp_mode, i1, j1, g1);
         const int kl = j0, ku = n - 1 - i1;        // largest ranks needed from either end
@@ -867,7 +910,55 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
             }
             ok = tl != HK_NONE && tu != HK_NONE;
         }
-        if (ok) {
+#if FM_HK_ABL == 1
+        if (ok) { lo = -1.0; hi = 1.0; fast_done = true; }
+        if (false) {
+#else
+        if (ok && FM_HK_WAVELIST) {
+#endif
+            // candidates straight into per-wave lists: wave w writes its lower-tail rows to
+            // cidx[64 w ..] and its upper-tail rows to cidx[LCAP + 64 w ..] (re-indexed into
+            // 64-candidate runs at the gather below), no count pass for list offsets first.  A wave holding more than 64
+            // candidates of a tail, or too many in all, falls back to the counted compaction
+            // (with the threshold refinement) below.
+            int wl = 0, wh = 0;
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+                uint32_t k = hk[v];
+                asm volatile("" : "+v"(k));
+                const bool bl = k <= tl, bh = HK_MAX - k <= tu;
+                const uint64_t ml = __ballot(bl), mh = __ballot(bh);
+                const int row = hk_row(v, tid);
+                if (ml) {   // wave-uniform
+                    const int p = wl + mask_rank(ml);
+                    if (bl && p < WAVE) sm.cidx[w * WAVE + p] = row;
+                    wl += (int)__popcll(ml);
+                }
+                if (mh) {
+                    const int p = wh + mask_rank(mh);
+                    if (bh && p < WAVE) sm.cidx[LCAP + w * WAVE + p] = row;
+                    wh += (int)__popcll(mh);
+                }
+            }
+            if (lane == 0) {
+                sm.wc[0][w] = wl;
+                sm.wc[1][w] = wh;
+            }
+            __syncthreads();
+            bool over = false;
+            clo = chi = 0;
+#pragma unroll
+            for (int q = 0; q < LNW; ++q) {
+                const int a0 = sm.wc[0][q], a1 = sm.wc[1][q];
+                over = over || a0 > WAVE || a1 > WAVE;
+                clo += a0;
+                chi += a1;
+            }
+            fast_done = !over && clo + chi <= n && clo > kl && chi > ku;   // block-uniform
+            if (fast_done) cand = true;
+            else __syncthreads();   // every read of sm.wc above before the counted path rewrites it
+        }
+        if (ok && !fast_done) {
             // candidates: key <= tl (a prefix of the sorted values) / HK_MAX - key <= tu (a
             // suffix); NaN keys fail both (the subtraction wraps them above every tu)
             int ol = 0, oh = LCAP;
@@ -939,7 +1030,7 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
                     asm volatile("" : "+v"(k));
                     const bool bl = k <= tl, bh = HK_MAX - k <= tu;
                     const uint64_t ml = __ballot(bl), mh = __ballot(bh);
-                    const int row = tid + v * LT;
+                    const int row = hk_row(v, tid);
                     if (ml) {   // wave-uniform: most value slots hold no candidate
                         if (bl) sm.cidx[ol + mask_rank(ml)] = row;
                         ol += (int)__popcll(ml);
@@ -954,19 +1045,36 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
             }
         }
     }
+#if FM_HK_ABL == 2
+    if (cand) { lo = -1.0; hi = 1.0; cand = false; }
+#endif
     if (cand) {   // block-uniform
         // gather the candidates' full values (a few hundred rows of the unit just read); wave
         // w sorts run w of each tail (64 keys; the upper tail on complemented keys), then every
         // candidate's merged rank = its run position + the entries of the other runs before it.
         // (Ordering the candidates by (high key, row) first and gathering only the tie groups at
         // the target ranks measured slower: 0.91-1.0 vs 0.66 ms on 1,000 x 20,000 x 15.)
+        // candidate e of the merged list: cidx[e], or with per-wave runs the (e - prefix)-th
+        // entry of the last wave whose count prefix is <= e (scalar prefixes, a few selects)
         const int e = w * WAVE + lane;
         const int nrl = __builtin_amdgcn_readfirstlane((clo + WAVE - 1) / WAVE);
         const int nru = __builtin_amdgcn_readfirstlane((chi + WAVE - 1) / WAVE);
-        const int rl = e < clo ? sm.cidx[e] : 0, ru = e < chi ? sm.cidx[LCAP + e] : 0;
+        int il = e, iu = e;
+        if (fast_done) {   // block-uniform
+            int pl = 0, pu = 0;
+#pragma unroll
+            for (int q = 0; q < LNW; ++q) {
+                if (e >= pl) il = e + (q * WAVE - pl);
+                if (e >= pu) iu = e + (q * WAVE - pu);
+                pl += sm.wc[0][q];
+                pu += sm.wc[1][q];
+            }
+        }
+        const bool vl = e < clo, vu = e < chi;
+        const int rl = vl ? sm.cidx[il] : 0, ru = vu ? sm.cidx[LCAP + iu] : 0;
         const double xl = col[rl], xu = col[ru];
-        uint64_t ka[1] = {e < clo ? dkey(xl) : SENT};
-        uint64_t kb[1] = {e < chi ? ~dkey(xu) : SENT};
+        uint64_t ka[1] = {vl ? dkey(xl) : SENT};
+        uint64_t kb[1] = {vu ? ~dkey(xu) : SENT};
         if (w < nrl) wave_sort<1>(ka);
         if (w < nru) wave_sort<1>(kb);
         sm.ck[e] = ka[0];
