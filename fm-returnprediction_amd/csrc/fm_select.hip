@@ -735,6 +735,12 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
 #ifndef FM_HK_ABL
 #define FM_HK_ABL 0   // timing ablations only (wrong cuts): 1 = stop after the thresholds, 2 = before the gather, 3 = after the counts
 #endif
+#ifndef FM_HK_KTH
+#define FM_HK_KTH 1   // per-wave thresholds by bit bisection (not a sort of the thread keys)
+#endif
+#ifndef FM_HK_SORT64
+#define FM_HK_SORT64 1   // candidate runs sorted with the lane-mask 64-bit bitonic network
+#endif
 #ifndef FM_HK_WAVELIST
 #define FM_HK_WAVELIST 1   // long-month candidates written straight into per-wave runs (no count pass)
 #endif
@@ -825,6 +831,13 @@ __device__ __forceinline__ void hk_load_plane(const uint32_t* hp, int L, uint32_
     }
 }
 
+// v with lane Q's value replaced by the uniform x (one v_writelane)
+template <int Q>
+__device__ __forceinline__ int writelane(int v, int x) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(Q));
+    return v;
+}
+
 // One (month, column) unit whose raw high words are in hk.
 template <int VPT>
 __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t (&hk)[VPT], LongHkSmem& sm) {
@@ -883,6 +896,14 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
         ok = ql <= WAVE && qu <= WAVE;
         uint32_t tl = HK_NONE, tu = HK_NONE;
         if (ok) {
+#if FM_HK_KTH
+            uint32_t ta, tb;   // the ql-th / qu-th smallest lane key, by bisection
+            wave_kth_u32x2(ua, ql, ub, qu, ta, tb);
+            if (lane == 0) {
+                sm.tw[0][w] = ta;
+                sm.tw[1][w] = tb;
+            }
+#else
             uint32_t ha[1] = {ua}, hb[1] = {ub};
             wave_sort32<1>(ha);
             wave_sort32<1>(hb);
@@ -890,16 +911,21 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
                 sm.tw[0][w] = (uint32_t)__builtin_amdgcn_readlane((int)ha[0], ql - 1);
                 sm.tw[1][w] = (uint32_t)__builtin_amdgcn_readlane((int)hb[0], qu - 1);
             }
+#endif
             __syncthreads();
-#pragma unroll
-            for (int q = 0; q < LNW; ++q) {
+            // this wave's count under each wave's threshold, lane q holding threshold q's, one
+            // LDS add per lane (a threshold of HK_NONE is never taken: its count is moot)
+            int pa = 0, pb = 0;
+            static_for<0, LNW>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
                 const uint32_t Ta = sm.tw[0][q], Tb = sm.tw[1][q];
-                const int ca = (int)__popcll(__ballot(ua != HK_NONE && ua <= Ta));
-                const int cb = (int)__popcll(__ballot(ub != HK_NONE && ub <= Tb));
-                if (lane == 0) {
-                    atomicAdd(&sm.tot[0][q], ca);
-                    atomicAdd(&sm.tot[1][q], cb);
-                }
+                const int ca = (int)__popcll(__ballot(ua <= Ta)), cb = (int)__popcll(__ballot(ub <= Tb));
+                pa = writelane<q>(pa, ca);
+                pb = writelane<q>(pb, cb);
+            });
+            if (lane < LNW) {
+                atomicAdd(&sm.tot[0][lane], pa);
+                atomicAdd(&sm.tot[1][lane], pb);
             }
             __syncthreads();
 #pragma unroll
@@ -921,22 +947,24 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
             // 64-candidate runs at the gather below), no count pass for list offsets first.  A wave holding more than 64
             // candidates of a tail, or too many in all, falls back to the counted compaction
             // (with the threshold refinement) below.
+            // (a wave past 64 candidates wraps inside its own list: the unit then takes the
+            // counted path below, which rewrites every list)
             int wl = 0, wh = 0;
 #pragma unroll
             for (int v = 0; v < VPT; ++v) {
-                uint32_t k = hk[v];
-                asm volatile("" : "+v"(k));
+                const uint32_t k = hk[v];
                 const bool bl = k <= tl, bh = HK_MAX - k <= tu;
                 const uint64_t ml = __ballot(bl), mh = __ballot(bh);
-                const int row = hk_row(v, tid);
                 if (ml) {   // wave-uniform
-                    const int p = wl + mask_rank(ml);
-                    if (bl && p < WAVE) sm.cidx[w * WAVE + p] = row;
+                    const int p = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)ml, (uint32_t)wl));
+                    if (bl) sm.cidx[w * WAVE + (p & (WAVE - 1))] = hk_row(v, tid);
                     wl += (int)__popcll(ml);
                 }
                 if (mh) {
-                    const int p = wh + mask_rank(mh);
-                    if (bh && p < WAVE) sm.cidx[LCAP + w * WAVE + p] = row;
+                    const int p = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mh >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mh, (uint32_t)wh));
+                    if (bh) sm.cidx[LCAP + w * WAVE + (p & (WAVE - 1))] = hk_row(v, tid);
                     wh += (int)__popcll(mh);
                 }
             }
@@ -1075,25 +1103,35 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
         const double xl = col[rl], xu = col[ru];
         uint64_t ka[1] = {vl ? dkey(xl) : SENT};
         uint64_t kb[1] = {vu ? ~dkey(xu) : SENT};
+#if FM_HK_SORT64
+        if (w < nrl) wave_sort64<1>(ka);
+        if (w < nru) wave_sort64<1>(kb);
+#else
         if (w < nrl) wave_sort<1>(ka);
         if (w < nru) wave_sort<1>(kb);
+#endif
         sm.ck[e] = ka[0];
         sm.ck[LCAP + e] = kb[0];
         if (tid < 4) sm.res[tid] = SENT;
         __syncthreads();
+        // both tails' searches of run u side by side (independent LDS chains); a run past a
+        // tail's count is all SENT and adds 0; SENT lanes count garbage and store nothing
+        const int nr = nrl > nru ? nrl : nru;
+        int ra = lane, rb = lane;
+#pragma unroll
+        for (int u = 0; u < LNW; ++u) {
+            if (u < nr && u != w) {   // wave-uniform
+                ra += merge_count(sm.ck + u * WAVE, ka[0], u < w);
+                rb += merge_count(sm.ck + LCAP + u * WAVE, kb[0], u < w);
+            }
+        }
         if (ka[0] != SENT) {
-            int r = lane;
-            for (int u = 0; u < nrl; ++u)
-                if (u != w) r += merge_count(sm.ck + u * WAVE, ka[0], u < w);
-            if (r == i0) sm.res[0] = ka[0];
-            if (r == j0) sm.res[1] = ka[0];
+            if (ra == i0) sm.res[0] = ka[0];
+            if (ra == j0) sm.res[1] = ka[0];
         }
         if (kb[0] != SENT) {
-            int r = lane;
-            for (int u = 0; u < nru; ++u)
-                if (u != w) r += merge_count(sm.ck + LCAP + u * WAVE, kb[0], u < w);
-            if (r == n - 1 - i1) sm.res[2] = ~kb[0];
-            if (r == n - 1 - j1) sm.res[3] = ~kb[0];
+            if (rb == n - 1 - i1) sm.res[2] = ~kb[0];
+            if (rb == n - 1 - j1) sm.res[3] = ~kb[0];
         }
         __syncthreads();
         lo = qlerp(kval(sm.res[0]), kval(sm.res[1]), g0, a.lerp_mode);

@@ -378,6 +378,62 @@ __device__ __forceinline__ void wave_sort32(uint32_t (&v)[R]) {
     if constexpr (K < WAVE * R) wave_sort32<R, K * 2>(v);
 }
 
+// 64-bit keys, the same scheme: the partner by DPP / permlane (per 32-bit half), ONE 64-bit
+// compare into a lane mask, and the lane's role as a compile-time mask -- a lane takes the
+// partner iff (partner < own) == (the lane keeps the minimum): an s_xnor and two v_cndmask
+// per register and stage (the generic wave_sort spends lane arithmetic and four selects).
+template <int R, int K, int J>
+__device__ __forceinline__ void bitonic_u64_stages(uint64_t (&v)[R]) {
+    if constexpr (J >= WAVE) {
+        constexpr int rj = J / WAVE;
+        static_for<0, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            if constexpr ((r & rj) == 0) {
+                constexpr bool up = ((WAVE * r) & K) == 0;
+                const uint64_t a = v[r], b = v[r | rj];
+                const uint64_t mn = a < b ? a : b, mx = a < b ? b : a;
+                v[r] = up ? mn : mx;
+                v[r | rj] = up ? mx : mn;
+            }
+        });
+    } else {
+        static_for<0, R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            const uint64_t p = xor_lane<J>(v[r]);
+            const uint64_t lt = __ballot(p < v[r]);
+            const uint64_t take = ~(lt ^ lane_mask<bitonic_min_mask<K, J, r>()>());
+            const uint32_t lo = cnd_u32(take, (uint32_t)v[r], (uint32_t)p);
+            const uint32_t hi = cnd_u32(take, (uint32_t)(v[r] >> 32), (uint32_t)(p >> 32));
+            v[r] = ((uint64_t)hi << 32) | lo;
+        });
+    }
+    if constexpr (J > 1) bitonic_u64_stages<R, K, J / 2>(v);
+}
+
+// One wave sorts its 64 R 64-bit keys ascending (element e = lane + 64 r in register r); the
+// whole wave must be active (the compare is a ballot).
+template <int R, int K = 2>
+__device__ __forceinline__ void wave_sort64(uint64_t (&v)[R]) {
+    bitonic_u64_stages<R, K, K / 2>(v);
+    if constexpr (K < WAVE * R) wave_sort64<R, K * 2>(v);
+}
+
+// The q-th smallest (1-based, q <= 64) of the wave's lane keys a, and the r-th of b: MSB-first
+// bisection on the key bits, one ballot count per bit and key (uniform results; no sort)
+__device__ __forceinline__ void wave_kth_u32x2(uint32_t a, int q, uint32_t b, int r, uint32_t& ka, uint32_t& kb) {
+    uint32_t ta = 0, tb = 0;
+#pragma unroll
+    for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t m = (1u << bit) - 1u;
+        const int ca = (int)__popcll(__ballot(a <= (ta | m)));
+        const int cb = (int)__popcll(__ballot(b <= (tb | m)));
+        ta |= ca < q ? (1u << bit) : 0u;
+        tb |= cb < r ? (1u << bit) : 0u;
+    }
+    ka = ta;
+    kb = tb;
+}
+
 // Element e (wave-uniform, < 64 R) of a wave-distributed u32 array: one readlane per register,
 // the register picked by scalar selects.
 template <int R>
