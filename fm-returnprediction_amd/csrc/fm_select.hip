@@ -735,11 +735,11 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
 #ifndef FM_HK_ABL
 #define FM_HK_ABL 0   // timing ablations only (wrong cuts): 1 = stop after the thresholds, 2 = before the gather, 3 = after the counts
 #endif
+#ifndef FM_PAIR_KTH
+#define FM_PAIR_KTH 1   // pair select: the tail threshold by bisection over unsorted lane extremes
+#endif
 #ifndef FM_HK_KTH
 #define FM_HK_KTH 1   // per-wave thresholds by bit bisection (not a sort of the thread keys)
-#endif
-#ifndef FM_HK_SORT64
-#define FM_HK_SORT64 1   // candidate runs sorted with the lane-mask 64-bit bitonic network
 #endif
 #ifndef FM_HK_WAVELIST
 #define FM_HK_WAVELIST 1   // long-month candidates written straight into per-wave runs (no count pass)
@@ -1103,13 +1103,8 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
         const double xl = col[rl], xu = col[ru];
         uint64_t ka[1] = {vl ? dkey(xl) : SENT};
         uint64_t kb[1] = {vu ? ~dkey(xu) : SENT};
-#if FM_HK_SORT64
-        if (w < nrl) wave_sort64<1>(ka);
-        if (w < nru) wave_sort64<1>(kb);
-#else
         if (w < nrl) wave_sort<1>(ka);
         if (w < nru) wave_sort<1>(kb);
-#endif
         sm.ck[e] = ka[0];
         sm.ck[LCAP + e] = kb[0];
         if (tid < 4) sm.res[tid] = SENT;
@@ -1834,8 +1829,10 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
         const bool amb = tvalid && (kmn == 0u || kmx == HK_MAX);
         {
             uint32_t ta[1] = {tvalid ? kmn : HK_NONE}, tb[1] = {tvalid ? HK_MAX - kmx : HK_NONE};
+#if !FM_PAIR_KTH
             wave_sort32<1>(ta);
             wave_sort32<1>(tb);
+#endif
             sm.sk[h][0][lane] = ta[0];
             sm.sk[h][1][lane] = tb[0];
         }
@@ -1860,6 +1857,10 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
             const int t = h;
             const int kr = t == 0 ? j0 : n - 1 - i1;
             uint32_t T = HK_NONE;
+#if FM_PAIR_KTH
+            // (unsorted lane extremes of both halves; the (kr+1)-th smallest by bisection)
+            if (kr < 2 * WAVE) T = wave_kth_u32_of2(sm.sk[0][t][lane], sm.sk[1][t][lane], kr + 1);
+#else
             if (kr < 2 * WAVE) {
                 const uint32_t mine = sm.sk[0][t][lane], other = sm.sk[1][t][lane];
                 const int q0 = lane + count_below_u32(sm.sk[1][t], mine, false);
@@ -1868,6 +1869,7 @@ __global__ __launch_bounds__(2 * WAVE, pair_hk_wgs(VPH) / 2) void select_pair_hk
                 if (m0) T = (uint32_t)__builtin_amdgcn_readlane((int)mine, __builtin_ctzll(m0));
                 else if (m1) T = (uint32_t)__builtin_amdgcn_readlane((int)other, __builtin_ctzll(m1));
             }
+#endif
             if (lane == 0) {
                 sm.tv[h] = T;
                 sm.okv[h] = T <= HK_MAX ? 1 : 0;

@@ -200,42 +200,6 @@ __device__ __forceinline__ void radix_pair(const double (&xv)[VPT], int ri, int 
     kj = le >= rj + 1 ? ki : nxt;
 }
 
-// Bitonic sort (ascending) of the 64*R keys held by one wave: element e = lane + 64*r lives
-// in register r of lane e&63.  Cross-lane stages exchange through DPP / permlane; the j=64
-// stage of R=2 is register-local.
-template <int R>
-__device__ __forceinline__ void wave_sort(uint64_t (&v)[R]) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int k = 2; k <= WAVE * R; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= WAVE) {
-                const int rj = j / WAVE;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (r & rj) continue;
-                    const bool up = (((lane + WAVE * r) & k) == 0);
-                    const uint64_t a = v[r], b = v[r | rj];
-                    const uint64_t mn = a < b ? a : b, mx = a < b ? b : a;
-                    v[r] = up ? mn : mx;
-                    v[r | rj] = up ? mx : mn;
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const uint64_t p = xor_lanes_u64(v[r], j);
-                    const bool up = (((lane + WAVE * r) & k) == 0);
-                    const bool lower = (lane & j) == 0;
-                    const bool take_min = lower == up;
-                    const uint64_t mn = p < v[r] ? p : v[r], mx = p < v[r] ? v[r] : p;
-                    v[r] = take_min ? mn : mx;
-                }
-            }
-        }
-    }
-}
-
 // Bitonic stage (k, j) for register r (element e = lane + 64 r): lane l keeps the minimum
 // iff ((l & j) == 0) == ((e & k) == 0).  As a compile-time 64-bit lane mask the role costs
 // one s_mov_b64 instead of per-stage lane arithmetic.
@@ -416,6 +380,26 @@ template <int R, int K = 2>
 __device__ __forceinline__ void wave_sort64(uint64_t (&v)[R]) {
     bitonic_u64_stages<R, K, K / 2>(v);
     if constexpr (K < WAVE * R) wave_sort64<R, K * 2>(v);
+}
+
+// The q-th smallest (1-based, q <= 128) of the 128 keys a, b held by the wave's lanes: the
+// same bisection, two ballot counts per bit
+__device__ __forceinline__ uint32_t wave_kth_u32_of2(uint32_t a, uint32_t b, int q) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t m = t | ((1u << bit) - 1u);
+        const int c = (int)__popcll(__ballot(a <= m)) + (int)__popcll(__ballot(b <= m));
+        t |= c < q ? (1u << bit) : 0u;
+    }
+    return t;
+}
+
+// Bitonic sort (ascending) of the 64*R keys held by one wave (element e = lane + 64*r in
+// register r); the whole wave active
+template <int R>
+__device__ __forceinline__ void wave_sort(uint64_t (&v)[R]) {
+    wave_sort64<R>(v);
 }
 
 // The q-th smallest (1-based, q <= 64) of the wave's lane keys a, and the r-th of b: MSB-first
