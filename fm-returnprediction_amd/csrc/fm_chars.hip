@@ -135,6 +135,9 @@ __global__ __launch_bounds__(CT) void firm_chars_kernel(fm_chars_args a, int nee
 // ---- rolling std --------------------------------------------------------------------------
 // tile shape (timing builds may override): 256 x 8 measured best -- 512 x 8 0.116, 256 x 16
 // 0.119, 512 x 4 0.179, 1024 x 4 0.205 vs 0.111 ms (profiles/r04/v11_stdbench_tile_sweep.log)
+#ifndef FM_STD_ABL
+#define FM_STD_ABL 0   // timing ablations only (wrong output): 1 no division / sqrt, 2 no first-window block sum, 3 staging + block stats only
+#endif
 #ifndef FM_STD_T
 #define FM_STD_T 256
 #endif
@@ -280,17 +283,53 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
     double* bmean = (double*)(fb + nw);
     double* bm2 = bmean + NB;
     int* bcnt = (int*)(bm2 + NB);
+    // 4-block superblock states (NB is a multiple of 16) and 1 / (c (c - 1)) for c <= W
+    const int NS = NB / 4;
+    double* smean = (double*)(bcnt + NB);
+    double* sm2 = smean + NS;
+    int* scnt = (int*)(sm2 + NS);
+    double* ivar = (double*)(scnt + NS);
     for (int s = threadIdx.x; s < NB; s += ST_T) {
         const RunStats st = range_stats(xs, HP + (s - nh) * ST_R, HP + (s - nh + 1) * ST_R);
         bmean[s] = st.mean;
         bm2[s] = st.m2;
         bcnt[s] = st.n;
     }
+    for (int c = threadIdx.x; c <= W; c += ST_T) ivar[c] = c >= 2 ? 1.0 / ((double)c * ((double)c - 1.0)) : 0.0;
+    __syncthreads();
+    // superblock = four block states merged (Chan et al.: M2 = sum M2_i + n_i (mean_i - mean)^2)
+    for (int S = threadIdx.x; S < NS; S += ST_T) {
+        int c = 0;
+        double sx = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            c += bcnt[4 * S + i];
+            sx += (double)bcnt[4 * S + i] * bmean[4 * S + i];
+        }
+        const double mean = c > 0 ? sx / (double)c : 0.0;
+        double m2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const double d = bmean[4 * S + i] - mean;
+            m2 += bm2[4 * S + i] + (double)bcnt[4 * S + i] * d * d;
+        }
+        smean[S] = mean;
+        sm2[S] = m2;
+        scnt[S] = c;
+    }
     __syncthreads();
     const int t = threadIdx.x;
     const int e0 = HP + t * ST_R;   // staged index of this thread's first row
     const int64_t i0 = b + t * ST_R;
     if (i0 >= n) return;
+#if FM_STD_ABL == 3
+    if (i0 + ST_R <= n) {
+#pragma unroll
+        for (int r = 0; r < ST_R; r += 2)
+            *reinterpret_cast<double2*>(out + i0 + r) = make_double2(xs[spad(e0 + r)] + bm2[t], xs[spad(e0 + r + 1)]);
+    }
+    return;
+#endif
     // first window: staged rows [lo, e0], lo = max(e0 - H, the firm's first row): the highest
     // firm-start bit at or below e0 (fs = -1 when the firm starts before the window)
     const int lo0 = e0 - H;
@@ -328,19 +367,30 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
         add_state(range_stats(xs, lo, HP + jlo * ST_R));
         int c4[4] = {0, 0, 0, 0};
         double a4[4] = {0.0, 0.0, 0.0, 0.0}, q4[4] = {0.0, 0.0, 0.0, 0.0};
-        int j = jlo;
-        for (; j + 3 < t; j += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int s = j + u + nh;
-                const double d = bmean[s] - K;
-                const double nd = (double)bcnt[s] * d;
-                c4[u] += bcnt[s];
-                a4[u] += nd;
-                q4[u] += bm2[s] + nd * d;
-            }
+        auto acc4 = [&](int u, int c, double mean, double m2) {
+            const double d = mean - K;
+            const double nd = (double)c * d;
+            c4[u] += c;
+            a4[u] += nd;
+            q4[u] += m2 + nd * d;
+        };
+        // blocks jlo .. t-1 as single blocks up to a superblock boundary, whole superblocks
+        // (two chains), then single blocks: ~W / 32 + 6 states instead of ~W / 8
+        int s = jlo + nh;
+        const int se = t + nh;
+#if FM_STD_ABL == 2
+        s = se;
+#endif
+        for (; s < se && (s & 3) != 0; ++s) acc4(2, bcnt[s], bmean[s], bm2[s]);
+        for (; s + 8 <= se; s += 8) {
+            acc4(0, scnt[s >> 2], smean[s >> 2], sm2[s >> 2]);
+            acc4(1, scnt[(s >> 2) + 1], smean[(s >> 2) + 1], sm2[(s >> 2) + 1]);
         }
-        for (; j < t; ++j) add_state(RunStats{bcnt[j + nh], bmean[j + nh], bm2[j + nh]});
+        if (s + 4 <= se) {
+            acc4(0, scnt[s >> 2], smean[s >> 2], sm2[s >> 2]);
+            s += 4;
+        }
+        for (; s < se; ++s) acc4(3, bcnt[s], bmean[s], bm2[s]);
         cnt += (c4[0] + c4[1]) + (c4[2] + c4[3]);
         s1 += (a4[0] + a4[1]) + (a4[2] + a4[3]);
         s2 += (q4[0] + q4[1]) + (q4[2] + q4[3]);
@@ -405,8 +455,14 @@ __global__ __launch_bounds__(ST_T) void rolling_std_kernel(const int64_t* __rest
                 rv = 0.0;   // pandas: every observation in the window is the same value
             } else {
                 const double c = (double)cnt;
-                const double var = (s2 * c - s1 * s1) / (c * (c - 1.0));
+#if FM_STD_ABL == 1
+                rv = (s2 * c - s1 * s1) * scale;
+#else
+                // the division by c (c - 1) as a product with its tabled reciprocal (within an
+                // ulp of the quotient)
+                const double var = (s2 * c - s1 * s1) * ivar[cnt];
                 rv = sqrt(var > 0.0 ? var : 0.0) * scale;
+#endif
             }
         }
         res[r] = rv;
@@ -477,7 +533,8 @@ extern "C" int fm_rolling_std(const int64_t* ids, const double* x, int64_t n, in
     FM_REQUIRE(min_periods >= 1 && min_periods <= window, "fm_rolling_std: min_periods must be 1..window");
     const int E = ST_ROWS + st_halo(window);
     const int nb = ST_T + st_halo(window) / ST_R;
-    const size_t lds = (size_t)(spad(E) + 1) * 8 + (size_t)((E + 63) / 64) * 8 + (size_t)nb * (8 * 2 + 4);
+    const size_t lds = (size_t)(spad(E) + 1) * 8 + (size_t)((E + 63) / 64) * 8 + (size_t)nb * (8 * 2 + 4) +
+                       (size_t)(nb / 4) * (8 * 2 + 4) + (size_t)(window + 1) * 8;
     FM_REQUIRE(lds <= 160 * 1024, "fm_rolling_std: window too large for LDS");
     const int64_t blocks = (n + ST_ROWS - 1) / ST_ROWS;
     FM_REQUIRE(blocks < (1ll << 31), "fm_rolling_std: too many rows");
