@@ -157,7 +157,7 @@ __global__ __launch_bounds__(ET) void gen_kernel(uint64_t seed, int64_t month0, 
     nyse[cell] = cell_hash(seed, m, f, 66) < nyse_thr ? 1 : 0;
 }
 
-// The achievable HBM READ rate (bench.py's measured_copy_peak for the read-dominated Gram):
+// The achievable HBM READ rate (bench.py's measured_read_peak for the read-dominated Gram):
 // 16-byte loads, PU of them in flight per thread, grid-stride over the buffer; the sum keeps
 // the loads.  n must be a multiple of 2 (double2 pairs) for the full rate; an odd tail is
 // read by thread 0.
@@ -181,6 +181,26 @@ __global__ __launch_bounds__(ET) void probe_kernel(const double* __restrict__ sr
     if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) s += src[n - 1];
     s = block_sum<ET / WAVE>(s, red);
     if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+// The achievable HBM COPY rate (read + write bytes): the same grid-stride 16-byte stream,
+// each pair stored to dst (bench.py's measured_copy_peak).  An odd tail by thread 0.
+__global__ __launch_bounds__(ET) void copy_probe_kernel(const double* __restrict__ src, double* __restrict__ dst,
+                                                        int64_t n) {
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+    double2* d2 = reinterpret_cast<double2*>(dst);
+    const int64_t np = n / 2;
+    const int64_t stride = (int64_t)gridDim.x * ET;
+    int64_t i = (int64_t)blockIdx.x * ET + threadIdx.x;
+    for (; i + (PU - 1) * stride < np; i += PU * stride) {
+        double2 v[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) v[u] = s2[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) d2[i + u * stride] = v[u];
+    }
+    for (; i < np; i += stride) d2[i] = s2[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) dst[n - 1] = src[n - 1];
 }
 
 // The FP64 panel as two 32-bit planes (high words, low words): the selects order values by
@@ -364,5 +384,16 @@ extern "C" int fm_stream_probe(const double* src, int64_t n, double* out, void* 
     FM_REQUIRE(((uintptr_t)src & 15) == 0, "fm_stream_probe: src must be 16-byte aligned");
     hipLaunchKernelGGL(probe_kernel, dim3(256 * 8), dim3(ET), 0, (hipStream_t)stream, src, n, out);
     FM_CHECK_LAUNCH("fm_stream_probe");
+    return FM_OK;
+}
+
+extern "C" int fm_stream_copy_probe(const double* src, double* dst, int64_t n, void* stream) {
+    using namespace fm;
+    FM_REQUIRE(src && dst, "fm_stream_copy_probe: null pointer");
+    FM_REQUIRE((((uintptr_t)src | (uintptr_t)dst) & 15) == 0, "fm_stream_copy_probe: src and dst must be 16-byte aligned");
+    FM_REQUIRE(n >= 0, "fm_stream_copy_probe: negative n");
+    if (n == 0) return FM_OK;
+    hipLaunchKernelGGL(copy_probe_kernel, dim3(256 * 8), dim3(ET), 0, (hipStream_t)stream, src, dst, n);
+    FM_CHECK_LAUNCH("fm_stream_copy_probe");
     return FM_OK;
 }

@@ -148,6 +148,7 @@ _SIGS = {
     "fm_gen_panel_planes": (_i32, [C.c_uint64, _i64, _i32, _i32, _f64, _f64, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     "fm_merge_planes": (_i32, [_p, _p, _i64, _i32, _i64, _p, _i64, _p]),
     "fm_stream_probe": (_i32, [_p, _i64, _p, _p]),
+    "fm_stream_copy_probe": (_i32, [_p, _p, _i64, _p]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -1271,3 +1271,18 @@ def stream_probe(t):
     _kcall("fm_stream_probe", "fm_stream_probe", *args, _stream())
     LAST_LAUNCH["fm_stream_probe"] = ("fm_stream_probe", None, ((t, out), args))
     return out
+
+
+def stream_copy_probe(src, dst):
+    """fm_stream_copy_probe: dst <- src (contiguous, 16-byte aligned float64 tensors of one
+    size) as the probe's 16-byte stream (bench.py's measured copy rate; re-issued by
+    time_launch)."""
+    for t in (src, dst):
+        if t.dtype != torch.float64 or not t.is_contiguous() or t.data_ptr() % 16:
+            raise ValueError("stream_copy_probe: contiguous, 16-byte aligned float64 tensors")
+    if src.numel() != dst.numel() or src.device != dst.device:
+        raise ValueError("stream_copy_probe: src and dst must match in size and device")
+    args = (src.data_ptr(), dst.data_ptr(), src.numel())
+    _kcall("fm_stream_copy_probe", "fm_stream_copy_probe", *args, _stream())
+    LAST_LAUNCH["fm_stream_copy_probe"] = ("fm_stream_copy_probe", None, ((src, dst), args))
+    return dst

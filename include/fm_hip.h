@@ -504,6 +504,9 @@ int fm_merge_planes(const uint32_t* hi, const uint32_t* lo, int64_t plane_stride
 int fm_split_planes(const double* cols, int64_t col_stride, int32_t ncols, int64_t nrows, uint32_t* hi,
                     uint32_t* lo, int64_t plane_stride, void* stream);
 int fm_stream_probe(const double* src, int64_t n, double* out, void* stream);
+/* Copy n doubles src -> dst as the probe's 16-byte stream (measures the HBM copy rate;
+ * bench.py's measured_copy_peak).  src / dst 16-byte aligned, not overlapping. */
+int fm_stream_copy_probe(const double* src, double* dst, int64_t n, void* stream);
 
 /* fm_ffill_expand: records sorted by (group, month code) with CSR rec_off[ngroups+1];
  * out_off[ngroups+1] is the prefix of each group's output month count (planned by the

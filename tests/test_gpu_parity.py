@@ -1734,3 +1734,16 @@ def test_planes_stale_after_in_place_write_refused(E):
         E.select_cuts(p, 0.01, 0.99, 5, E.LERP_NUMPY)
     E.split_planes(p)
     E.select_cuts(p, 0.01, 0.99, 5, E.LERP_NUMPY)
+
+
+def test_stream_probes_read_and_copy(E):
+    """bench.py's measured read / copy peaks come from fm_stream_probe / fm_stream_copy_probe:
+    the read probe sums every element (odd tail included), the copy probe copies them."""
+    import torch
+    for n in (1, 7, 4096 * 1024 + 3):
+        src = torch.arange(n, dtype=torch.float64, device="cuda") * 0.5 - 3.0
+        s = E.stream_probe(src)
+        assert abs(float(s.item()) - float(src.sum().item())) <= 1e-9 * max(1.0, float(src.abs().sum().item()))
+        dst = torch.full_like(src, float("nan"))
+        E.stream_copy_probe(src, dst)
+        assert torch.equal(dst, src)
