@@ -718,11 +718,14 @@ __global__ __launch_bounds__(LT, MID ? 3 : 4) void select_long_kernel(SelArgs a)
 // every step before the final candidate sort works on the HIGH 32 bits of the values' order
 // keys (thread extrema, per-wave thresholds, ballot counts, compaction), and only the
 // candidates' full values are gathered back from memory (a few hundred per unit).  40 VGPRs
-// of keys per thread: three workgroups per CU.  The grid is persistent: once a unit's
-// candidates are compacted its key registers are dead, so the next unit's loads are issued
-// right behind the candidate gather and fly during the sort and merge (measured on 1,000 x
-// 20,000 x 15: up to the compaction 0.42 ms, the gather +0.12 ms, sort +0.07, merge +0.05
-// when each unit waited for its own gather).
+// of keys per thread: three workgroups per CU, one unit each.  Per unit (round 6): the keys
+// stream in as 16-byte slots (four rows per lane); each wave's tail threshold is its lane
+// keys' q-th smallest by bit bisection; the candidates go straight into per-wave lists (no
+// counting pass) and are re-indexed into 64-entry runs at the gather; the runs are sorted
+// by the lane-mask 64-bit network and ranked by binary searches of the other runs, both
+// tails side by side.  The SIMDs issue VALU in ~70 % of the kernel's cycles
+// (profiles/r06/v11-v12): stage ablations on 1,000 x 20,000 x 15 put load + keys + counts at
+// 0.21 ms of 0.48.
 //
 // (Thresholds from each thread's two smallest / largest keys instead of one measured slower:
 // 0.72 vs 0.64 ms -- three more wave sorts per tail cost more than the fewer candidates save.)
@@ -944,11 +947,10 @@ __device__ __forceinline__ void hk_unit(const SelArgs& a, int s, int c, uint32_t
 #endif
             // candidates straight into per-wave lists: wave w writes its lower-tail rows to
             // cidx[64 w ..] and its upper-tail rows to cidx[LCAP + 64 w ..] (re-indexed into
-            // 64-candidate runs at the gather below), no count pass for list offsets first.  A wave holding more than 64
-            // candidates of a tail, or too many in all, falls back to the counted compaction
-            // (with the threshold refinement) below.
-            // (a wave past 64 candidates wraps inside its own list: the unit then takes the
-            // counted path below, which rewrites every list)
+            // 64-candidate runs at the gather below), no count pass for list offsets first.  A
+            // wave holding more than 64 candidates of a tail (its writes wrap inside its own
+            // list), or too many in all, sends the unit to the counted compaction with the
+            // threshold refinement below, which rewrites every list.
             int wl = 0, wh = 0;
 #pragma unroll
             for (int v = 0; v < VPT; ++v) {
