@@ -1747,3 +1747,46 @@ def test_stream_probes_read_and_copy(E):
         dst = torch.full_like(src, float("nan"))
         E.stream_copy_probe(src, dst)
         assert torch.equal(dst, src)
+
+
+@pytest.mark.parametrize("layout", ["f64", "planes"])
+def test_long_month_tails_crowded_into_one_wave(E, layout):
+    """The long-month kernel writes each wave's tail candidates into a 64-entry list of its
+    own; a wave holding more than that sends the unit to the counted compaction.  Rows
+    r with (r mod 2,048) < 256 are one wave's (16-byte slots: four rows per lane, 512 lanes);
+    here every tail value of a month sits in them (and in another month in the last wave's
+    rows), so the fallback runs -- bit-exact against np.percentile either way."""
+    rng = np.random.default_rng(11)
+    n = 20000
+    rows = np.arange(n)
+    segs = []
+    for lo_w, hi_w in ((0, 0), (7, 7), (0, 7), (3, 3)):
+        x = rng.standard_normal(n)
+        order = np.argsort(x)
+        k = 400                                      # > 64 per tail, 1 % ranks at ~200
+        low_rows = rows[(rows % 2048) // 256 == lo_w]
+        high_rows = rows[(rows % 2048) // 256 == hi_w]
+        xs = x[order]
+        y = np.empty(n)
+        taken = np.zeros(n, dtype=bool)
+        sel_lo = rng.choice(low_rows, k, replace=False)
+        y[sel_lo] = xs[:k]
+        taken[sel_lo] = True
+        free_hi = high_rows[~taken[high_rows]]
+        sel_hi = rng.choice(free_hi, k, replace=False)
+        y[sel_hi] = xs[-k:]
+        taken[sel_hi] = True
+        rest = rows[~taken]
+        y[rest] = rng.permutation(xs[k:n - k])
+        segs.append(y)
+    segs.append(rng.standard_normal(n))               # an ordinary month beside them
+    vals = np.concatenate(segs)
+    labels = np.repeat(np.arange(len(segs)), [len(s) for s in segs])
+    panel = E.panel_from_arrays([vals], ["v"], labels, layout=layout)
+    assert panel.max_seg_len == n
+    for qa, qb in ((1, 99), (2, 98)):
+        cuts = E.select_cuts(panel, qa / 100, qb / 100, 1, E.LERP_NUMPY, center=True)
+        lo, hi = cuts.lo.cpu().numpy()[0], cuts.hi.cpu().numpy()[0]
+        for t, s in enumerate(segs):
+            ra, rb = np.percentile(s, qa), np.percentile(s, qb)
+            assert _same([lo[t]], [ra]) and _same([hi[t]], [rb]), (layout, qa, t, lo[t], ra, hi[t], rb)
