@@ -47,8 +47,8 @@ def parse(argv=None):
                     help="ranks (one per GPU); without WORLD_SIZE in the environment, N > 1 starts "
                          "N worker processes itself through torch.distributed.run (default: "
                          "WORLD_SIZE, else 1)")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=("headline", "c5"), default=None,
                     help="default: headline at N=1, c5 at N>1")
     ap.add_argument("--months", type=int, default=600, help="headline months per GPU")

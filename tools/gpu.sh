@@ -15,7 +15,7 @@ for s in "$@"; do
     parity)  specs+=("parity:::600:::$PT -m gpu tests/test_gpu_parity.py");;
     dist)    specs+=("dist:::400:::$PT -m gpu tests/test_gpu_dist.py tests/test_gpu_rccl.py");;
     smoke)   specs+=("smoke:::200:::python -c 'import __graft_entry__ as g; g.smoke()'");;
-    bench)   specs+=("bench:::500:::python bench.py --steps 20 $BENCH_ARGS");;
+    bench)   specs+=("bench:::500:::python bench.py $BENCH_ARGS");;
     quick)   specs+=("quick:::300:::python bench.py --no-cpu --no-chars --no-c5 --steps 20 $BENCH_ARGS");;
     scan)    specs+=("scan:::300:::python tools/size_scan.py");;
     split)   specs+=("split:::300:::python tools/split_scan.py");;
