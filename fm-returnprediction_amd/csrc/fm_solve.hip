@@ -374,6 +374,18 @@ __global__ __launch_bounds__(VT) void solve_kernel(fm_solve_args a) {
 // factorizations run in the time of one.  Rank-deficient problems (rare) take the Jacobi
 // pseudo-inverse path one at a time.
 
+#ifndef FM_SOLVE_RSQ
+#define FM_SOLVE_RSQ 1
+#endif
+// 1 / sqrt(x) for a positive normal x: v_rsq_f64 refined by two Newton steps
+__device__ __forceinline__ double rsq_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
 template <int L>
 __device__ __forceinline__ int rowbc_i(int v) {   // lane L of this lane's 16-lane row
     // every lane has a source (row_newbcast): mov_dpp needs no zero-initialised destination
@@ -583,8 +595,15 @@ __global__ __launch_bounds__(S16T, 3) void solve16_kernel(fm_solve_args a) {
             const bool bad = act && (!(orig > 0.0) || !(piv > CHOL_REL * orig));
             if (bad) ok = false;
             const bool go = act && !bad;
+#if FM_SOLVE_RSQ
+            // 1 / sqrt(piv) by the hardware estimate and two Newton steps (error ~1 ulp), sqrt
+            // as piv times it: no IEEE sqrt and division sequences on the pivot chain
+            const double rinv = rsq_nr(piv);
+            const double lkk = piv * rinv;
+#else
             const double lkk = sqrt(piv);
             const double rinv = 1.0 / lkk;
+#endif
             const double lik = row[k] * rinv;
             // unguarded: the entries a guard would keep are never read again -- columns past
             // the problem's K (and, once k >= K, everything this step touches) are not used by
